@@ -1,0 +1,474 @@
+// knn.hip -- exact k-nearest-neighbour classification for gfx950 (CDNA4), VALU only.
+//
+// Replaces KNeighborsClassifier(n_neighbors=k).fit/predict/kneighbors as used by
+// src/models.py:33-35,52-58 (sklearn 1.7.2: algorithm='auto' -> kd_tree, minkowski p=2,
+// uniform weights, scipy.stats.mode vote).
+//
+// Pipeline (all stream-ordered, no host sync):
+//   1. knn_convert    fp64 [N,D] -> fp32 [N,DP] zero-padded rows (+ max row norm^2, for the bound)
+//   2. knn_screen     grid (query block of 256, reference split): each thread owns one query,
+//                     streams its split's reference rows through LDS tiles and keeps the KC
+//                     smallest fp32 squared distances (KC = k + 4 slack) in registers.  The
+//                     [Nq x Nr] distance matrix is never materialised.
+//   3. knn_merge      one thread per query: re-ranks every surviving candidate with the
+//                     reference's own fp64 distance (sequential sum of squared differences, no
+//                     FMA -- sklearn euclidean_rdist), keeps the k best by (distance, index), and
+//                     certifies that no screened-out row can beat the k-th; otherwise the query
+//                     goes on a fallback list.
+//   4. knn_fallback   one workgroup per listed query: exhaustive fp64 scan.
+//   5. vote           majority label, smallest label on ties (scipy.stats.mode).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dsp_audiorec.h"
+
+namespace dsp {
+
+static constexpr int KNN_TQ = 256;   // queries per screening workgroup (one per thread)
+static constexpr int KNN_TR = 256;   // reference rows per LDS tile
+static constexpr int KNN_SLACK = 4;  // extra screened candidates per split
+
+__global__ void knn_convert(const double *__restrict__ src, int64_t N, int D, int DP,
+                            float *__restrict__ dst, unsigned int *maxnorm_bits)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float nrm = 0.f;
+    if (i < N) {
+        for (int c = 0; c < DP; c++) {
+            float v = c < D ? (float)src[i * D + c] : 0.f;
+            dst[i * DP + c] = v;
+            nrm = fmaf(v, v, nrm);
+        }
+    }
+    // block max -> one atomic (non-negative floats order like their bit patterns)
+    for (int o = 32; o > 0; o >>= 1) nrm = fmaxf(nrm, __shfl_xor(nrm, o, 64));
+    if ((threadIdx.x & 63) == 0 && maxnorm_bits) atomicMax(maxnorm_bits, __float_as_uint(nrm));
+}
+
+// insert (d, r) into the ascending list (dl, il) of length KC if it beats the last entry
+template <int KC>
+__device__ __forceinline__ void topk_insert(float (&dl)[KC], int (&il)[KC], float d, int r)
+{
+    if (!(d < dl[KC - 1])) return;
+#pragma unroll
+    for (int i = KC - 1; i > 0; i--) {
+        const bool shift = d < dl[i - 1];
+        const bool here = !shift && d < dl[i];
+        if (shift) {
+            dl[i] = dl[i - 1];
+            il[i] = il[i - 1];
+        } else if (here) {
+            dl[i] = d;
+            il[i] = r;
+        }
+    }
+    if (d < dl[0]) {
+        dl[0] = d;
+        il[0] = r;
+    }
+}
+
+template <int DP, int KC>
+__global__ __launch_bounds__(KNN_TQ) void knn_screen(const float *__restrict__ ref32, int64_t Nr,
+                                                      const float *__restrict__ q32, int64_t Nq,
+                                                      int64_t self_offset, int nsplit,
+                                                      float *__restrict__ cand_d,
+                                                      int *__restrict__ cand_i)
+{
+    __shared__ __attribute__((aligned(16))) float tile[KNN_TR * DP];
+    const int qb = blockIdx.x, sp = blockIdx.y;
+    const int tid = threadIdx.x;
+    const int64_t q = (int64_t)qb * KNN_TQ + tid;
+    const int64_t per = (Nr + nsplit - 1) / nsplit;
+    const int64_t r0 = (int64_t)sp * per, r1 = min(Nr, r0 + per);
+    float qv[DP];
+#pragma unroll
+    for (int c = 0; c < DP; c++) qv[c] = q < Nq ? q32[q * DP + c] : 0.f;
+    const int64_t self = (self_offset >= 0 && q < Nq) ? self_offset + q : -1;
+    float dl[KC];
+    int il[KC];
+#pragma unroll
+    for (int i = 0; i < KC; i++) {
+        dl[i] = INFINITY;
+        il[i] = -1;
+    }
+    for (int64_t t0 = r0; t0 < r1; t0 += KNN_TR) {
+        const int nt = (int)min((int64_t)KNN_TR, r1 - t0);
+        __syncthreads();
+        // cooperative tile load: KNN_TR rows x DP floats, float4 granules
+        for (int e = tid; e < KNN_TR * DP / 4; e += KNN_TQ) {
+            const int row = e / (DP / 4);
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (row < nt) v = reinterpret_cast<const float4 *>(ref32 + (t0 + row) * DP)[e % (DP / 4)];
+            reinterpret_cast<float4 *>(tile)[e] = v;
+        }
+        __syncthreads();
+        for (int j = 0; j < nt; j++) {
+            const float4 *rv = reinterpret_cast<const float4 *>(tile + j * DP);
+            float d = 0.f;
+#pragma unroll
+            for (int c4 = 0; c4 < DP / 4; c4++) {
+                const float4 r = rv[c4];
+                float t;
+                t = qv[4 * c4 + 0] - r.x; d = fmaf(t, t, d);
+                t = qv[4 * c4 + 1] - r.y; d = fmaf(t, t, d);
+                t = qv[4 * c4 + 2] - r.z; d = fmaf(t, t, d);
+                t = qv[4 * c4 + 3] - r.w; d = fmaf(t, t, d);
+            }
+            const int64_t r = t0 + j;
+            if (r == self) d = INFINITY;
+            topk_insert<KC>(dl, il, d, (int)r);
+        }
+    }
+    if (q < Nq) {
+        const size_t o = ((size_t)sp * Nq + q) * KC;
+#pragma unroll
+        for (int i = 0; i < KC; i++) {
+            cand_d[o + i] = dl[i];
+            cand_i[o + i] = il[i];
+        }
+    }
+}
+
+#pragma clang fp contract(off)
+// sklearn euclidean_rdist: sequential d += t*t, no FMA
+__device__ __forceinline__ double rdist64(const double *__restrict__ a, const double *__restrict__ b, int D)
+{
+    double d = 0.0;
+    for (int c = 0; c < D; c++) {
+        const double t = a[c] - b[c];
+        d = d + t * t;
+    }
+    return d;
+}
+#pragma clang fp contract(on)
+
+__device__ __forceinline__ bool cand_less(double da, int ia, double db, int ib)
+{
+    return da < db || (da == db && ia < ib);
+}
+
+template <int K>
+__device__ __forceinline__ void topk64_insert(double (&dl)[K], int (&il)[K], int kk, double d, int r)
+{
+    if (!cand_less(d, r, dl[kk - 1], il[kk - 1])) return;
+#pragma unroll
+    for (int i = K - 1; i > 0; i--) {
+        if (i >= kk) continue;
+        const bool shift = cand_less(d, r, dl[i - 1], il[i - 1]);
+        const bool here = !shift && cand_less(d, r, dl[i], il[i]);
+        if (shift) {
+            dl[i] = dl[i - 1];
+            il[i] = il[i - 1];
+        } else if (here) {
+            dl[i] = d;
+            il[i] = r;
+        }
+    }
+    if (cand_less(d, r, dl[0], il[0])) {
+        dl[0] = d;
+        il[0] = r;
+    }
+}
+
+__device__ int vote(const int *il, int k, const int32_t *labels)
+{
+    int best = -1, bestc = 0;
+    for (int a = 0; a < k; a++) {
+        if (il[a] < 0) continue;
+        const int la = labels[il[a]];
+        int c = 0;
+        for (int b = 0; b < k; b++) c += il[b] >= 0 && labels[il[b]] == la;
+        if (c > bestc || (c == bestc && la < best)) {
+            bestc = c;
+            best = la;
+        }
+    }
+    return best;
+}
+
+static constexpr int KMAX = 32;
+
+template <int KC>
+__global__ void knn_merge(const double *__restrict__ ref, const double *__restrict__ query,
+                          int64_t Nr, int64_t Nq, int D, int k, int nsplit, int64_t self_offset,
+                          const float *__restrict__ cand_d, const int *__restrict__ cand_i,
+                          const unsigned int *maxnorm_bits, const int32_t *__restrict__ labels,
+                          int32_t *__restrict__ idx, double *__restrict__ dist,
+                          int32_t *__restrict__ pred, int *fb_count, int *fb_list)
+{
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= Nq) return;
+    const double *qx = query + q * D;
+    double dl[KMAX];
+    int il[KMAX];
+#pragma unroll
+    for (int i = 0; i < KMAX; i++) {
+        dl[i] = INFINITY;
+        il[i] = 0x7fffffff;
+    }
+    double qn = 0.0;
+    for (int c = 0; c < D; c++) qn += qx[c] * qx[c];
+    // screening cut-off of every split whose candidate list is full
+    float cut = INFINITY;
+    for (int s = 0; s < nsplit; s++) {
+        const size_t o = ((size_t)s * Nq + q) * KC;
+        for (int i = 0; i < KC; i++) {
+            const int r = cand_i[o + i];
+            if (r < 0) continue;
+            if (self_offset >= 0 && r == self_offset + q) continue;
+            topk64_insert<KMAX>(dl, il, k, rdist64(qx, ref + (int64_t)r * D, D), r);
+        }
+        if (cand_i[o + KC - 1] >= 0) cut = fminf(cut, cand_d[o + KC - 1]);
+    }
+    // certification: any row that was screened out has fp32 distance >= cut; its true fp64
+    // squared distance is >= cut - tol (fp32 rounding of inputs and of the sum).
+    const double rmax = (double)__uint_as_float(*maxnorm_bits);
+    const double tol = 2e-6 * (double)cut + 1e-6 * (qn + rmax) + 1e-30;
+    const bool ok = !(cut < INFINITY) || ((double)cut - tol > dl[k - 1]);
+    if (!ok) {
+        const int slot = atomicAdd(fb_count, 1);
+        fb_list[slot] = (int)q;
+        return;
+    }
+    int outi[KMAX];
+    for (int i = 0; i < k; i++) {
+        const bool valid = dl[i] < INFINITY;
+        outi[i] = valid ? il[i] : -1;
+        idx[q * k + i] = outi[i];
+        dist[q * k + i] = valid ? sqrt(dl[i]) : INFINITY;
+    }
+    if (pred && labels) pred[q] = vote(outi, k, labels);
+}
+
+// exhaustive fp64 for the queries the screen could not certify: one workgroup per query
+static constexpr int FB_T = 256;
+__global__ __launch_bounds__(FB_T) void knn_fallback(const double *__restrict__ ref,
+                                                     const double *__restrict__ query, int64_t Nr,
+                                                     int D, int k, int64_t self_offset,
+                                                     const int *fb_count, const int *fb_list,
+                                                     const int32_t *__restrict__ labels,
+                                                     int32_t *__restrict__ idx,
+                                                     double *__restrict__ dist,
+                                                     int32_t *__restrict__ pred)
+{
+    __shared__ double sd[FB_T / 2 * KMAX];
+    __shared__ int si[FB_T / 2 * KMAX];
+    const int cnt = *fb_count;
+    const int tid = threadIdx.x;
+    for (int item = blockIdx.x; item < cnt; item += gridDim.x) {
+        const int64_t q = fb_list[item];
+        const double *qx = query + q * D;
+        double dl[KMAX];
+        int il[KMAX];
+#pragma unroll
+        for (int i = 0; i < KMAX; i++) {
+            dl[i] = INFINITY;
+            il[i] = 0x7fffffff;
+        }
+        for (int64_t r = tid; r < Nr; r += FB_T) {
+            if (self_offset >= 0 && r == self_offset + q) continue;
+            topk64_insert<KMAX>(dl, il, k, rdist64(qx, ref + r * D, D), (int)r);
+        }
+        // pairwise tree merge of the per-thread lists through LDS
+        for (int width = FB_T; width > 1; width >>= 1) {
+            const int half = width >> 1;
+            __syncthreads();
+            if (tid >= half && tid < width)
+                for (int i = 0; i < k; i++) {
+                    sd[(tid - half) * KMAX + i] = dl[i];
+                    si[(tid - half) * KMAX + i] = il[i];
+                }
+            __syncthreads();
+            if (tid < half)
+                for (int i = 0; i < k; i++)
+                    topk64_insert<KMAX>(dl, il, k, sd[tid * KMAX + i], si[tid * KMAX + i]);
+        }
+        if (tid == 0) {
+            int outi[KMAX];
+            for (int i = 0; i < k; i++) {
+                const bool valid = dl[i] < INFINITY;
+                outi[i] = valid ? il[i] : -1;
+                idx[q * k + i] = outi[i];
+                dist[q * k + i] = valid ? sqrt(dl[i]) : INFINITY;
+            }
+            if (pred && labels) pred[q] = vote(outi, k, labels);
+        }
+        __syncthreads();
+    }
+}
+
+// ---- z-score (src/feature_extraction.py:157-181), numpy axis-0 order ---------------------
+#pragma clang fp contract(off)
+__global__ void zscore_fit_kernel(const double *X, int64_t N, int D, double *mean, double *std)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= D) return;
+    double s = 0.0;
+    for (int64_t i = 0; i < N; i++) s = s + X[i * D + c];
+    const double m = s / (double)N;
+    double v = 0.0;
+    for (int64_t i = 0; i < N; i++) {
+        const double t = X[i * D + c] - m;
+        v = v + t * t;
+    }
+    const double sd = sqrt(v / (double)N);
+    mean[c] = m;
+    std[c] = sd == 0.0 ? 1.0 : sd;
+}
+
+__global__ void zscore_apply_kernel(const double *X, int64_t N, int D, const double *mean,
+                                    const double *std, double *out)
+{
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= N * D) return;
+    const int c = (int)(e % D);
+    out[e] = (X[e] - mean[c]) / std[c];
+}
+#pragma clang fp contract(on)
+
+}  // namespace dsp
+
+// ------------------------------------------------------------------------------------------
+namespace {
+struct KnnLayout {
+    size_t ref32, q32, cand_d, cand_i, misc, total;
+    int DP, KC, nsplit;
+};
+
+int pick_kc(int k)
+{
+    const int need = k + dsp::KNN_SLACK;
+    if (need <= 8) return 8;
+    if (need <= 16) return 16;
+    if (need <= 24) return 24;
+    return 36;
+}
+
+int pick_nsplit(int64_t Nr, int64_t Nq)
+{
+    const int64_t qblocks = (Nq + dsp::KNN_TQ - 1) / dsp::KNN_TQ;
+    int64_t s = (2048 + qblocks - 1) / qblocks;           // aim for >= 2048 workgroups
+    const int64_t maxs = (Nr + dsp::KNN_TR - 1) / dsp::KNN_TR;  // >= one tile per split
+    if (s > maxs) s = maxs;
+    if (s > 64) s = 64;
+    if (s < 1) s = 1;
+    return (int)s;
+}
+
+size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+
+KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
+{
+    KnnLayout l;
+    l.DP = D <= 16 ? 16 : 32;
+    l.KC = pick_kc(k);
+    l.nsplit = pick_nsplit(Nr, Nq);
+    size_t o = 0;
+    l.ref32 = o; o += al((size_t)Nr * l.DP * 4);
+    l.q32 = o;   o += al((size_t)Nq * l.DP * 4);
+    l.cand_d = o; o += al((size_t)l.nsplit * Nq * l.KC * 4);
+    l.cand_i = o; o += al((size_t)l.nsplit * Nq * l.KC * 4);
+    l.misc = o;  o += al(16 + (size_t)Nq * 4);   // maxnorm bits, fallback count, fallback list
+    l.total = o;
+    return l;
+}
+
+template <int DP, int KC>
+void launch_screen(dim3 g, hipStream_t s, const float *r, int64_t Nr, const float *q, int64_t Nq,
+                   int64_t self, int nsplit, float *cd, int *ci)
+{
+    hipLaunchKernelGGL((dsp::knn_screen<DP, KC>), g, dim3(dsp::KNN_TQ), 0, s, r, Nr, q, Nq, self,
+                       nsplit, cd, ci);
+}
+
+template <int KC>
+void launch_merge(dim3 g, dim3 b, hipStream_t s, const double *ref, const double *query,
+                  int64_t Nr, int64_t Nq, int D, int k, int nsplit, int64_t self, const float *cd,
+                  const int *ci, const unsigned *mx, const int32_t *lbl, int32_t *idx, double *dist,
+                  int32_t *pred, int *fbc, int *fbl)
+{
+    hipLaunchKernelGGL((dsp::knn_merge<KC>), g, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self,
+                       cd, ci, mx, lbl, idx, dist, pred, fbc, fbl);
+}
+}  // namespace
+
+extern "C" size_t dsp_knn_workspace_bytes(int64_t Nr, int64_t Nq, int D, int k)
+{
+    if (Nr < 0 || Nq < 0 || D < 1 || D > 32 || k < 1 || k > 32) return 0;
+    return knn_layout(Nr, Nq, D, k).total;
+}
+
+extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, int64_t Nr,
+                                const double *query, int64_t Nq, int D, int k, int64_t self_offset,
+                                int n_classes, int32_t *idx, double *dist, int32_t *pred,
+                                void *workspace, size_t workspace_bytes, void *stream)
+{
+    if (D < 1 || D > 32 || k < 1 || k > dsp::KMAX || Nr < 0 || Nq < 0) return DSP_ERR_ARGS;
+    if (Nr > 0x7fffffff || (Nq > 0 && (!query || !idx || !dist)) || (Nr > 0 && !ref))
+        return DSP_ERR_ARGS;
+    if (Nq == 0) return DSP_OK;
+    (void)n_classes;
+    const KnnLayout l = knn_layout(Nr, Nq, D, k);
+    if (!workspace || workspace_bytes < l.total) return DSP_ERR_WORKSPACE;
+    hipStream_t s = (hipStream_t)stream;
+    char *ws = (char *)workspace;
+    float *ref32 = (float *)(ws + l.ref32);
+    float *q32 = (float *)(ws + l.q32);
+    float *cd = (float *)(ws + l.cand_d);
+    int *ci = (int *)(ws + l.cand_i);
+    unsigned *mx = (unsigned *)(ws + l.misc);
+    int *fbc = (int *)(ws + l.misc + 4);
+    int *fbl = (int *)(ws + l.misc + 16);
+    if (hipMemsetAsync(ws + l.misc, 0, 16, s) != hipSuccess) return DSP_ERR_HIP;
+    const int cb = 256;
+    if (Nr > 0)
+        hipLaunchKernelGGL(dsp::knn_convert, dim3((unsigned)((Nr + cb - 1) / cb)), dim3(cb), 0, s,
+                           ref, Nr, D, l.DP, ref32, mx);
+    hipLaunchKernelGGL(dsp::knn_convert, dim3((unsigned)((Nq + cb - 1) / cb)), dim3(cb), 0, s,
+                       query, Nq, D, l.DP, q32, (unsigned *)nullptr);
+    const dim3 g((unsigned)((Nq + dsp::KNN_TQ - 1) / dsp::KNN_TQ), (unsigned)l.nsplit);
+#define DSP_SCREEN(DPV, KCV)                                                                  \
+    if (l.DP == DPV && l.KC == KCV) launch_screen<DPV, KCV>(g, s, ref32, Nr, q32, Nq, self_offset, \
+                                                            l.nsplit, cd, ci)
+    DSP_SCREEN(16, 8); DSP_SCREEN(16, 16); DSP_SCREEN(16, 24); DSP_SCREEN(16, 36);
+    DSP_SCREEN(32, 8); DSP_SCREEN(32, 16); DSP_SCREEN(32, 24); DSP_SCREEN(32, 36);
+#undef DSP_SCREEN
+    const int32_t *lbl = pred ? ref_labels : nullptr;
+    const dim3 mg((unsigned)((Nq + 127) / 128)), mb(128);
+    switch (l.KC) {
+    case 8: launch_merge<8>(mg, mb, s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, lbl, idx, dist, pred, fbc, fbl); break;
+    case 16: launch_merge<16>(mg, mb, s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, lbl, idx, dist, pred, fbc, fbl); break;
+    case 24: launch_merge<24>(mg, mb, s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, lbl, idx, dist, pred, fbc, fbl); break;
+    default: launch_merge<36>(mg, mb, s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, lbl, idx, dist, pred, fbc, fbl); break;
+    }
+    const unsigned fbgrid = (unsigned)(Nq < 512 ? Nq : 512);
+    hipLaunchKernelGGL(dsp::knn_fallback, dim3(fbgrid), dim3(dsp::FB_T), 0, s, ref, query, Nr, D,
+                       k, self_offset, fbc, fbl, lbl, idx, dist, pred);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? DSP_OK : DSP_ERR_HIP + (int)e;
+}
+
+extern "C" int dsp_zscore_fit(const double *X, int64_t N, int D, double *mean, double *std,
+                              void *stream)
+{
+    if (!X || !mean || !std || N < 1 || D < 1) return DSP_ERR_ARGS;
+    hipLaunchKernelGGL(dsp::zscore_fit_kernel, dim3((D + 63) / 64), dim3(64), 0,
+                       (hipStream_t)stream, X, N, D, mean, std);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? DSP_OK : DSP_ERR_HIP + (int)e;
+}
+
+extern "C" int dsp_zscore_apply(const double *X, int64_t N, int D, const double *mean,
+                                const double *std, double *out, void *stream)
+{
+    if (!X || !mean || !std || !out || N < 0 || D < 1) return DSP_ERR_ARGS;
+    if (N == 0) return DSP_OK;
+    const int64_t tot = N * D;
+    hipLaunchKernelGGL(dsp::zscore_apply_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, X, N, D, mean, std, out);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? DSP_OK : DSP_ERR_HIP + (int)e;
+}
+
+extern "C" int dsp_abi_version(void) { return DSP_ABI_VERSION; }

@@ -1,0 +1,101 @@
+"""ctypes binding of the gfx950 C-ABI library (include/dsp_audiorec.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (csrc/Makefile) into
+``dsp-audioreclabs_amd/lib/libdsp_audiorec.so``.  There is no CPU fallback: if the
+library or a HIP device is missing, every accelerated entry point raises.
+PyTorch is used only for device memory and the current stream.
+"""
+import ctypes
+import os
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libdsp_audiorec.so")
+
+DSP_OK = 0
+DSP_ERR_ARGS = 1
+DSP_ERR_TOO_LONG = 2
+DSP_ERR_WORKSPACE = 3
+DSP_ERR_HIP = 1000
+
+CLIP_OK = 0
+CLIP_EMPTY = 1
+CLIP_NO_AUDIO = 2
+CLIP_NO_FRAMES = 3
+CLIP_TOO_LONG = 4
+CLIP_FLAG_VAD_EXACT = 0x100
+
+EXPORTS = ("dsp_extract_lds_bytes", "dsp_extract_features", "dsp_knn_workspace_bytes",
+           "dsp_knn_classify", "dsp_zscore_fit", "dsp_zscore_apply", "dsp_abi_version")
+
+_lib = None
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def load_library(path=LIB_PATH):
+    """Load and type the C ABI (no GPU needed just to load)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:
+        # Load PyTorch's HIP runtime first: the library's DT_NEEDED libamdhip64.so.7 then binds to
+        # that same runtime (matching soname), so device pointers and streams are shared.  Without
+        # torch the library uses /opt/rocm's runtime on its own.
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not os.path.exists(path):
+        raise HipError("HIP extension not built (%s missing): run "
+                       "`python -c 'import __graft_entry__ as g; g.build()'` in the repo root" % path)
+    L = ctypes.CDLL(path)
+    vp, i64, i32, dbl, sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double, ctypes.c_size_t
+    L.dsp_extract_lds_bytes.restype = sz
+    L.dsp_extract_lds_bytes.argtypes = [i64, i32, i32]
+    L.dsp_extract_features.restype = i32
+    L.dsp_extract_features.argtypes = [vp, vp, i32, i64, i32, i32, vp, i32, dbl, dbl, dbl,
+                                       vp, vp, vp, vp, vp, vp, i32, vp, i32, vp]
+    L.dsp_knn_workspace_bytes.restype = sz
+    L.dsp_knn_workspace_bytes.argtypes = [i64, i64, i32, i32]
+    L.dsp_knn_classify.restype = i32
+    L.dsp_knn_classify.argtypes = [vp, vp, i64, vp, i64, i32, i32, i64, i32, vp, vp, vp, vp, sz, vp]
+    L.dsp_zscore_fit.restype = i32
+    L.dsp_zscore_fit.argtypes = [vp, i64, i32, vp, vp, vp]
+    L.dsp_zscore_apply.restype = i32
+    L.dsp_zscore_apply.argtypes = [vp, i64, i32, vp, vp, vp, vp]
+    L.dsp_abi_version.restype = i32
+    L.dsp_abi_version.argtypes = []
+    _lib = L
+    return L
+
+
+def lib():
+    return load_library()
+
+
+def require_device():
+    """The HIP device every accelerated call runs on; raises when there is none."""
+    import torch
+    if not torch.cuda.is_available():
+        raise HipError("no HIP device visible: the DSP hot path runs only on an MI355X (gfx950)")
+    load_library()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_handle(device=None):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def check(rc, what):
+    if rc != DSP_OK:
+        if rc >= DSP_ERR_HIP:
+            raise HipError("%s: HIP launch failed (hipError %d)" % (what, rc - DSP_ERR_HIP))
+        names = {DSP_ERR_ARGS: "invalid arguments", DSP_ERR_TOO_LONG: "clip longer than the LDS pipeline",
+                 DSP_ERR_WORKSPACE: "workspace too small"}
+        raise HipError("%s: %s (code %d)" % (what, names.get(rc, "error"), rc))

@@ -1,0 +1,190 @@
+"""Batched device API of the hot path (PyTorch-ROCm tensors in, tensors out).
+
+This is what the reference's per-file loop becomes (experiments/run_experiments.py:78-111):
+a batch of int16 clips resident in HBM goes through one fused HIP launch
+(``dsp_extract_features``) and a 15-d feature matrix comes back, then
+``knn_classify`` runs KNeighborsClassifier's exact k-NN + vote on the device.
+"""
+import numpy as np
+
+from . import _hip
+
+FEATURE_NAMES = ["%s_%s" % (f, s) for f in ("energy", "magnitude", "zcr")
+                 for s in ("mean", "std", "max", "min", "median")]
+
+
+def create_window(window_type, length):
+    """src/audio_processing.py:278-296 -- host-side coefficients, exactly numpy's."""
+    if window_type == "rectangular":
+        return np.ones(length)
+    if window_type == "hamming":
+        return np.hamming(length)
+    if window_type == "hanning":
+        return np.hanning(length)
+    raise ValueError("不支持的窗函数类型: %s" % window_type)
+
+
+def _as_device(x, dtype, device):
+    import torch
+    if isinstance(x, torch.Tensor):
+        return x.to(device=device, dtype=dtype).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(x)).to(device=device, dtype=dtype).contiguous()
+
+
+class FeatureExtractor:
+    """Reusable launch plan for ``dsp_extract_features`` (outputs preallocated per batch size).
+
+    Parameters mirror process_audio_file (src/audio_processing.py:336-341) with frame sizes
+    in samples, as the reference's callers pass them (experiments/run_experiments.py:90-99).
+    """
+
+    def __init__(self, frame_length, frame_shift, window_type="hamming", do_endpoint_detection=True,
+                 energy_high_ratio=0.5, energy_low_ratio=0.1, zcr_threshold_ratio=1.5,
+                 return_vad_lists=False, return_sequences=False, device=None):
+        import torch
+        self.device = device or _hip.require_device()
+        self.L, self.S = int(frame_length), int(frame_shift)
+        if self.L < 1 or self.S < 1:
+            raise ValueError("frame_length and frame_shift must be positive")
+        self.window_type = window_type
+        self.window = torch.as_tensor(create_window(window_type, self.L), dtype=torch.float64).to(self.device)
+        self.do_vad = bool(do_endpoint_detection)
+        self.ratios = (float(energy_high_ratio), float(energy_low_ratio), float(zcr_threshold_ratio))
+        self.return_vad_lists = return_vad_lists
+        self.return_sequences = return_sequences
+        self._bufs = {}
+
+    def lds_bytes(self, max_len):
+        return _hip.lib().dsp_extract_lds_bytes(int(max_len), self.L, self.S)
+
+    def _outputs(self, B, max_len):
+        import torch
+        key = (B, max_len)
+        if key not in self._bufs:
+            d = self.device
+            o = dict(feat=torch.empty((B, 15), dtype=torch.float32, device=d),
+                     start_end=torch.empty((B, 2), dtype=torch.int32, device=d),
+                     n_frames=torch.empty(B, dtype=torch.int32, device=d),
+                     status=torch.empty(B, dtype=torch.int32, device=d))
+            if self.return_vad_lists:
+                ld = max(1, (max_len - self.L) // self.S + 1) if max_len >= self.L else 1
+                o["vad_energy"] = torch.zeros((B, ld), dtype=torch.float64, device=d)
+                o["vad_zcr"] = torch.zeros((B, ld), dtype=torch.int32, device=d)
+            if self.return_sequences:
+                ld = 1 if max_len <= self.L else (max_len - self.L + self.S - 1) // self.S + 1
+                o["seq"] = torch.zeros((B, ld, 3), dtype=torch.float32, device=d)
+            self._bufs = {key: o}  # keep one shape alive
+        return self._bufs[key]
+
+    def __call__(self, pcm, offsets=None, max_len=None):
+        """pcm: int16 [B, N] (uniform clips) or packed 1-D int16 with int64 offsets [B+1].
+
+        Returns a dict of device tensors: feat [B,15] f32, start_end [B,2] i32,
+        n_frames [B] i32, status [B] i32 (+ vad_energy/vad_zcr, seq when requested).
+        The tensors are reused by the next call with the same shape.
+        """
+        import torch
+        d = self.device
+        pcm = _as_device(pcm, torch.int16, d)
+        if offsets is None:
+            if pcm.dim() != 2:
+                raise ValueError("1-D packed pcm needs offsets")
+            B, N = pcm.shape
+            key = ("uni", B, N)
+            if key not in self._bufs:
+                self._bufs[key] = torch.arange(B + 1, dtype=torch.int64, device=d) * N
+            off = self._bufs[key]
+            max_len = N
+        else:
+            if isinstance(offsets, np.ndarray) or not isinstance(offsets, torch.Tensor):
+                off_h = np.asarray(offsets, dtype=np.int64)
+                if max_len is None:
+                    max_len = int(np.max(np.diff(off_h))) if off_h.size > 1 else 1
+            elif max_len is None:
+                max_len = int(torch.max(offsets[1:] - offsets[:-1]).item())
+            off = _as_device(offsets, torch.int64, d)
+            B = off.numel() - 1
+        pcm = pcm.reshape(-1)
+        max_len = max(int(max_len), 1)
+        out = self._outputs(B, max_len)
+        hi, lo, zr = self.ratios
+        ve, vz, ldv = out.get("vad_energy"), out.get("vad_zcr"), 0
+        if ve is not None:
+            ldv = ve.shape[1]
+        sq, lds_ = out.get("seq"), 0
+        if sq is not None:
+            lds_ = sq.shape[1]
+        rc = _hip.lib().dsp_extract_features(
+            _hip.ptr(pcm), _hip.ptr(off), B, max_len, self.L, self.S, _hip.ptr(self.window),
+            int(self.do_vad), hi, lo, zr, _hip.ptr(out["feat"]), _hip.ptr(out["start_end"]),
+            _hip.ptr(out["n_frames"]), _hip.ptr(out["status"]), _hip.ptr(ve), _hip.ptr(vz), ldv,
+            _hip.ptr(sq), lds_, _hip.stream_handle(d))
+        _hip.check(rc, "dsp_extract_features")
+        return out
+
+
+def process_audio_batch(pcm, offsets=None, frame_length=1102, frame_shift=441, window_type="hamming",
+                        do_endpoint_detection=True, energy_high_ratio=0.5, energy_low_ratio=0.1,
+                        zcr_threshold_ratio=1.5, return_vad_lists=False, return_sequences=False,
+                        max_len=None):
+    """One-shot batched form of process_audio_file + extract_features_from_frames."""
+    fx = FeatureExtractor(frame_length, frame_shift, window_type, do_endpoint_detection,
+                          energy_high_ratio, energy_low_ratio, zcr_threshold_ratio,
+                          return_vad_lists, return_sequences)
+    return dict(fx(pcm, offsets, max_len))
+
+
+def knn_classify(ref, ref_labels, query, k, self_offset=-1, n_classes=None, with_pred=True):
+    """Exact k-NN (KNeighborsClassifier semantics) on the device.
+
+    ref [Nr, D] / query [Nq, D] float64 (cast if needed), ref_labels int [Nr].
+    Returns (idx int32 [Nq,k], dist float64 [Nq,k], pred int32 [Nq] or None).
+    """
+    import torch
+    d = _hip.require_device()
+    ref = _as_device(ref, torch.float64, d)
+    q = _as_device(query, torch.float64, d)
+    Nr, D = ref.shape
+    Nq = q.shape[0]
+    lbl = _as_device(ref_labels, torch.int32, d) if (ref_labels is not None and with_pred) else None
+    if n_classes is None:
+        n_classes = 0
+    ws_bytes = _hip.lib().dsp_knn_workspace_bytes(Nr, Nq, D, k)
+    if ws_bytes == 0 and Nq > 0:
+        raise ValueError("unsupported KNN shape (1 <= D <= 32, 1 <= k <= 32)")
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=d)
+    idx = torch.empty((Nq, k), dtype=torch.int32, device=d)
+    dist = torch.empty((Nq, k), dtype=torch.float64, device=d)
+    pred = torch.empty(Nq, dtype=torch.int32, device=d) if lbl is not None else None
+    rc = _hip.lib().dsp_knn_classify(_hip.ptr(ref), _hip.ptr(lbl), Nr, _hip.ptr(q), Nq, D, k,
+                                     int(self_offset), int(n_classes), _hip.ptr(idx), _hip.ptr(dist),
+                                     _hip.ptr(pred), _hip.ptr(ws), ws_bytes, _hip.stream_handle(d))
+    _hip.check(rc, "dsp_knn_classify")
+    return idx, dist, pred
+
+
+def zscore_fit(X):
+    """normalize_features' mean/std (src/feature_extraction.py:171-177) on the device."""
+    import torch
+    d = _hip.require_device()
+    X = _as_device(X, torch.float64, d)
+    N, D = X.shape
+    mean = torch.empty(D, dtype=torch.float64, device=d)
+    std = torch.empty(D, dtype=torch.float64, device=d)
+    _hip.check(_hip.lib().dsp_zscore_fit(_hip.ptr(X), N, D, _hip.ptr(mean), _hip.ptr(std),
+                                         _hip.stream_handle(d)), "dsp_zscore_fit")
+    return mean, std
+
+
+def zscore_apply(X, mean, std):
+    import torch
+    d = _hip.require_device()
+    X = _as_device(X, torch.float64, d)
+    mean = _as_device(mean, torch.float64, d)
+    std = _as_device(torch.where(torch.as_tensor(std) == 0, 1.0, torch.as_tensor(std, dtype=torch.float64)),
+                     torch.float64, d)
+    out = torch.empty_like(X)
+    N, D = X.shape
+    _hip.check(_hip.lib().dsp_zscore_apply(_hip.ptr(X), N, D, _hip.ptr(mean), _hip.ptr(std), _hip.ptr(out),
+                                           _hip.stream_handle(d)), "dsp_zscore_apply")
+    return out

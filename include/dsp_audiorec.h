@@ -1,0 +1,130 @@
+/*
+ * dsp_audiorec.h -- C ABI of the MI355X (gfx950) feature-extraction + KNN path.
+ *
+ * Drop-in boundary for the reference's hot path (Hypersonic-cpu/DSP-AudioRecLabs):
+ * every entry point names the reference function(s) it replaces.  The reference is
+ * pure Python, so its "FFI" is the Python module surface src/audio_processing.py,
+ * src/feature_extraction.py and src/models.py; the host mirror of that surface
+ * (dsp-audioreclabs_amd/src/) binds this header with ctypes.
+ *
+ * Conventions
+ *  - All pointers are DEVICE pointers unless stated; buffers are caller-allocated.
+ *  - Every launch is stream-ordered on `stream` (a hipStream_t passed as void*;
+ *    NULL = the legacy default stream).  No entry point allocates, frees, copies
+ *    to the host or synchronises, so all of them may be captured in a hipGraph.
+ *  - Return value: 0 on success, a DSP_ERR_* code (argument checks, done on the
+ *    host before launching), or DSP_ERR_HIP + hipError_t when a launch fails.
+ *  - Per-item failures (the reference raises ValueError and its callers skip the
+ *    file, experiments/run_experiments.py:109-111) are reported in `status[b]`.
+ */
+#ifndef DSP_AUDIOREC_H
+#define DSP_AUDIOREC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSP_ABI_VERSION 1
+
+/* return codes */
+#define DSP_OK 0
+#define DSP_ERR_ARGS 1        /* bad sizes / null pointers / misaligned buffers */
+#define DSP_ERR_TOO_LONG 2    /* a clip does not fit the on-chip (LDS) pipeline */
+#define DSP_ERR_WORKSPACE 3   /* workspace too small */
+#define DSP_ERR_HIP 1000      /* + hipError_t of the failed launch */
+
+/* per-clip status[b] (low byte) -- same codes as the oracle */
+#define DSP_CLIP_OK 0
+#define DSP_CLIP_EMPTY 1      /* zero-length clip: np.max of an empty array raises (audio_processing.py:72) */
+#define DSP_CLIP_NO_AUDIO 2   /* "No audio remaining ..." (audio_processing.py:388-389) */
+#define DSP_CLIP_NO_FRAMES 3  /* "No frames provided ..." (feature_extraction.py:27-28) */
+#define DSP_CLIP_TOO_LONG 4   /* longer than the LDS capacity given at launch */
+/* status[b] flag bits (informational) */
+#define DSP_CLIP_FLAG_VAD_EXACT 0x100 /* endpoint decision was a near tie: re-decided on the
+                                         bit-exact (numpy-order) fp64 path */
+
+/* Bytes of dynamic LDS dsp_extract_features needs for clips of up to max_len samples
+ * (0 if it exceeds the 160 KiB of one CU). Host-only helper. */
+size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int frame_shift);
+
+/*
+ * dsp_extract_features -- fused per-clip pipeline, one workgroup per clip.
+ * Replaces, per clip, the chain
+ *   preprocess            src/audio_processing.py:78-90   (remove_dc :49-59, normalize_audio :62-75)
+ *   endpoint_detection    src/audio_processing.py:135-275 (when do_vad != 0)
+ *   crop                  src/audio_processing.py:378
+ *   frame_signal          src/audio_processing.py:299-333 (with create_window :278-296 supplied as `window`)
+ *   extract_frame_features src/feature_extraction.py:12-43
+ *   extract_statistical_features src/feature_extraction.py:65-88  (15-d vector)
+ * as called per file by experiments/run_experiments.py:90-104.
+ *
+ * pcm       int16 samples of all clips back to back; clip b = pcm[offsets[b] .. offsets[b+1]).
+ *           16-bit PCM as read by load_wav (:35-38); 8-bit PCM is passed as ((u8 - 128) mod 256),
+ *           which is what load_wav's uint8 arithmetic computes (:31-34) -- any power-of-two
+ *           scale cancels in preprocess.  `pcm` must be 16-byte aligned.
+ * offsets   int64 [B+1], non-decreasing.
+ * window    float64 [frame_length] = create_window(window_type, frame_length) (np.hamming etc.),
+ *           zero only at its ends (true for the three reference windows).
+ * hi/lo/zr  energy_high_ratio, energy_low_ratio, zcr_threshold_ratio (config.py:43-45).
+ * max_len   longest clip in the batch (sizes the LDS carve-up; see dsp_extract_lds_bytes).
+ * feat      float32 [B,15]: energy, magnitude, zcr x (mean, std, max, min, median).
+ * start_end int32 [B,2]: start_point / end_point (0, len when do_vad == 0).
+ * n_frames  int32 [B]: metadata['n_frames'] (frames after the crop).
+ * status    int32 [B]: DSP_CLIP_* | flags.
+ * vad_energy/vad_zcr (optional, may be NULL): float64 / int32 [B, ld_vad]: metadata energy_list,
+ *           zcr_list (first (len-L)//S+1 entries; rows of clips with len < L are untouched).
+ * seq       (optional, may be NULL): float32 [B, ld_seq, 3] per-frame (E, M, ZCR) -- the
+ *           'sequence' method of extract_features_from_frames (:114-129); frames beyond
+ *           ld_seq are dropped.
+ */
+int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, int B, int64_t max_len,
+                         int frame_length, int frame_shift, const double *window, int do_vad,
+                         double hi, double lo, double zr, float *feat, int32_t *start_end,
+                         int32_t *n_frames, int32_t *status, double *vad_energy,
+                         int32_t *vad_zcr, int ld_vad, float *seq, int ld_seq, void *stream);
+
+/*
+ * KNN -- KNeighborsClassifier(n_neighbors=k) as configured in src/models.py:33-35 and used by
+ * TraditionalClassifier.fit/predict (:52-58): exact Euclidean k nearest neighbours of each query
+ * row among the reference rows, ascending distance, then a uniform majority vote in which the
+ * smallest label wins ties (scipy.stats.mode).  Screening runs in fp32 on VALU (no MFMA);
+ * survivors are re-ranked with the reference's own fp64 distance (sequential sum of squared
+ * differences, no FMA, sqrt), and any query whose fp32 screen cannot certify the fp64 top-k is
+ * re-solved exhaustively in fp64 on the device.  Exact-distance ties are ordered by smaller
+ * reference index.
+ *
+ * ref        float64 [Nr, D] row-major,  ref_labels int32 [Nr] in [0, n_classes)
+ * query      float64 [Nq, D] row-major
+ * self_offset  >= 0: query q is reference row self_offset + q and is excluded from its own
+ *              neighbour list (kneighbors(X=None) semantics); -1: no exclusion.
+ * idx        int32 [Nq, k] (-1 where fewer than k candidates), dist float64 [Nq, k],
+ * pred       int32 [Nq] (may be NULL, or ref_labels NULL, to skip the vote)
+ * workspace  device scratch of dsp_knn_workspace_bytes(Nr, Nq, D, k) bytes.
+ * Requires 1 <= D <= 32, 1 <= k <= 32.
+ */
+size_t dsp_knn_workspace_bytes(int64_t Nr, int64_t Nq, int D, int k);
+int dsp_knn_classify(const double *ref, const int32_t *ref_labels, int64_t Nr, const double *query,
+                     int64_t Nq, int D, int k, int64_t self_offset, int n_classes, int32_t *idx,
+                     double *dist, int32_t *pred, void *workspace, size_t workspace_bytes,
+                     void *stream);
+
+/*
+ * normalize_features (src/feature_extraction.py:157-181): column mean and population std
+ * (ddof = 0, numpy axis-0 order: sequential over rows), std == 0 -> 1, then (X - mean) / std.
+ * dsp_zscore_fit writes mean/std [D] (std already with the 0 -> 1 substitution);
+ * dsp_zscore_apply writes out [N, D] (may alias X).  float64 throughout.
+ */
+int dsp_zscore_fit(const double *X, int64_t N, int D, double *mean, double *std, void *stream);
+int dsp_zscore_apply(const double *X, int64_t N, int D, const double *mean, const double *std,
+                     double *out, void *stream);
+
+/* ABI version of the loaded library (DSP_ABI_VERSION). */
+int dsp_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DSP_AUDIOREC_H */

@@ -1,0 +1,120 @@
+"""GPU parity of the fused extraction kernel against the reference goldens and the oracle.
+
+Tolerances (north star, BASELINE.json): start/end, n_frames and every ZCR value bit-exact;
+VAD energies within 1e-12 relative (float64 path); windowed per-frame E/M within 1e-5
+relative (fp32 path); 15-d statistics within 1e-5 relative plus 1e-6 x the magnitude of the
+sequence they summarise (a std of frames that are identical to the last bit is 0 in exact
+arithmetic and ~1e-16 x mean in float64: no implementation can match that digit).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import golden_clip, golden_keys
+
+pytestmark = pytest.mark.gpu
+
+
+def feat_close(got, ref):
+    got = np.asarray(got, np.float64).reshape(-1, 15)
+    ref = np.asarray(ref, np.float64).reshape(-1, 15)
+    scale = np.repeat(np.abs(ref[:, [0, 5, 10]]), 5, axis=1)
+    tol = 1e-5 * np.abs(ref) + 1e-6 * scale + 1e-30
+    bad = np.abs(got - ref) > tol
+    return bad
+
+
+@pytest.fixture(scope="module")
+def packed(golden):
+    import torch
+    pcm = golden["pcm"]
+    pad = np.zeros(8, np.int16)
+    t = torch.as_tensor(np.concatenate([pcm, pad])).cuda()
+    return t, golden["offsets"]
+
+
+def test_library_and_device():
+    from src import _hip
+    L = _hip.load_library()
+    assert L.dsp_abi_version() == 1
+    _hip.require_device()
+
+
+def test_golden_pipeline(golden, packed):
+    from src.pipeline import FeatureExtractor
+    pcm, off = packed
+    names = golden["clip_names"]
+    for key, L, S, wname, vad in golden_keys(golden):
+        fx = FeatureExtractor(L, S, wname, bool(vad), return_vad_lists=True, return_sequences=True)
+        out = {k: v.cpu().numpy() for k, v in fx(pcm, off).items()}
+        st = out["status"] & 0xFF
+        assert np.array_equal(st, golden[key + "/status"]), key
+        assert np.array_equal(out["n_frames"], golden[key + "/n_frames"]), key
+        if vad:
+            assert np.array_equal(out["start_end"], golden[key + "/start_end"]), (key, out["start_end"])
+        fo = golden[key + "/frame_off"]
+        for i in range(len(names)):
+            F = fo[i + 1] - fo[i]
+            seq = out["seq"][i, :F]
+            np.testing.assert_array_equal(seq[:, 2], golden[key + "/frame_zcr"][fo[i]:fo[i + 1]], err_msg=str((key, names[i])))
+            np.testing.assert_allclose(seq[:, 0], golden[key + "/frame_energy"][fo[i]:fo[i + 1]], rtol=1e-5, atol=1e-30, err_msg=str((key, names[i])))
+            np.testing.assert_allclose(seq[:, 1], golden[key + "/frame_magnitude"][fo[i]:fo[i + 1]], rtol=1e-5, atol=1e-30, err_msg=str((key, names[i])))
+            if vad:
+                vo = golden[key + "/vad_off"]
+                nv = vo[i + 1] - vo[i]
+                np.testing.assert_array_equal(out["vad_zcr"][i, :nv], golden[key + "/vad_zcr"][vo[i]:vo[i + 1]])
+                np.testing.assert_allclose(out["vad_energy"][i, :nv], golden[key + "/vad_energy"][vo[i]:vo[i + 1]], rtol=1e-12, atol=0)
+        bad = feat_close(out["feat"], golden[key + "/feat"])
+        assert not bad.any(), (key, [names[i] for i in np.nonzero(bad.any(1))[0]])
+
+
+@pytest.mark.parametrize("L,S,win", [(1102, 441, "hamming"), (1024, 512, "hamming"), (1102, 441, "hanning"),
+                                     (1102, 441, "rectangular"), (882, 220, "hamming"), (352, 441, "hamming"),
+                                     (2205, 441, "hanning")])
+def test_random_batch_vs_oracle(L, S, win):
+    import torch
+    from src.pipeline import FeatureExtractor, create_window
+    from src.synth import make_batch
+    B = 96
+    pcm = make_batch(B, base_seed=1000 + L + S)
+    fx = FeatureExtractor(L, S, win, True)
+    out = {k: v.cpu().numpy() for k, v in fx(torch.as_tensor(pcm).cuda()).items()}
+    ref = oracle.process_batch(pcm.reshape(-1), np.arange(B + 1) * pcm.shape[1], L, S, create_window(win, L), nthreads=8)
+    assert np.array_equal(out["start_end"], ref["start_end"])
+    assert np.array_equal(out["n_frames"], ref["n_frames"])
+    assert not feat_close(out["feat"], ref["feat"]).any()
+
+
+def test_vad_off_and_ragged():
+    import torch
+    from src.pipeline import FeatureExtractor, create_window
+    from src.synth import make_clip
+    rng = np.random.default_rng(3)
+    lens = [44100, 1, 0, 1101, 1102, 1103, 20000, 30001, 57000, 5, 44100]
+    clips = [make_clip(50 + i, n) if n > 0 else np.zeros(0, np.int16) for i, n in enumerate(lens)]
+    off = np.zeros(len(clips) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    pcm = np.concatenate(clips + [np.zeros(8, np.int16)])
+    for vad in (True, False):
+        fx = FeatureExtractor(1102, 441, "hamming", vad)
+        out = {k: v.cpu().numpy() for k, v in fx(torch.as_tensor(pcm).cuda(), off).items()}
+        for i, c in enumerate(clips):
+            r = oracle.process_clip(c, 1102, 441, create_window("hamming", 1102), do_vad=vad)
+            assert (out["status"][i] & 0xFF) == r["status"], i
+            if r["status"]:
+                assert np.isnan(out["feat"][i]).all()
+                continue
+            assert tuple(out["start_end"][i]) == (r["start"], r["end"]), (i, vad)
+            assert out["n_frames"][i] == r["n_frames"]
+            assert not feat_close(out["feat"][i], r["feat"]).any(), (i, vad, out["feat"][i], r["feat"])
+
+
+def test_too_long_status():
+    import torch
+    from src.pipeline import FeatureExtractor
+    from src.synth import make_clip
+    c = np.concatenate([make_clip(1, 44100), make_clip(2, 20000), np.zeros(8, np.int16)])
+    fx = FeatureExtractor(1102, 441, "hamming", True)
+    out = fx(torch.as_tensor(c).cuda(), np.array([0, 44100, 64100]), max_len=30000)
+    st = out["status"].cpu().numpy() & 0xFF
+    assert st[0] == 4 and st[1] == 0

@@ -52,14 +52,14 @@ def test_pipeline_bit_exact_vs_reference(golden):
 def test_float64_stereo_path(golden):
     from src.audio_processing import decode_pcm_bytes
     raw = golden["wav/u8_stereo/raw"]
-    x, _ = decode_pcm_bytes(raw.tobytes(), 1, 2)
+    x, _, _ = decode_pcm_bytes(raw.tobytes(), 1, 2)
     assert np.array_equal(x, golden["wav/u8_stereo/decoded"])
     win = np.hamming(1102)
     r = oracle.process_clip(x, 1102, 441, win)
     assert np.array_equal(r["feat"], golden["wav/u8_stereo/feat"])
     assert (r["start"], r["end"]) == tuple(golden["wav/u8_stereo/start_end"])
     raw = golden["wav/s16_stereo_clip/raw"]
-    x, _ = decode_pcm_bytes(raw.tobytes(), 2, 2)
+    x, _, _ = decode_pcm_bytes(raw.tobytes(), 2, 2)
     r = oracle.process_clip(x, 1102, 441, win)
     assert np.array_equal(r["feat"], golden["wav/s16_stereo_clip/feat"])
     assert (r["start"], r["end"]) == tuple(golden["wav/s16_stereo_clip/start_end"])
