@@ -9,7 +9,7 @@ import ctypes
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libdsp_audiorec.so")
+LIB_PATH = os.environ.get("DSP_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libdsp_audiorec.so")
 
 DSP_OK = 0
 DSP_ERR_ARGS = 1

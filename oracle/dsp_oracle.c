@@ -35,6 +35,37 @@
 #include "dsp_oracle.h"
 
 /* ------------------------------------------------------------------------ */
+/* per-thread LIFO scratch arena: no malloc/free (and no page faults) per clip */
+/* ------------------------------------------------------------------------ */
+static __thread char *tl_buf;
+static __thread size_t tl_cap, tl_top;
+
+/* called by public entry points before any allocation; grows only when idle */
+static void ws_reserve(size_t bytes)
+{
+    if (tl_top == 0 && bytes > tl_cap) {
+        free(tl_buf);
+        tl_buf = (char *)malloc(bytes);
+        tl_cap = bytes;
+    }
+}
+static size_t ws_round(size_t bytes) { return (bytes + 63) & ~(size_t)63; }
+static double *ws_alloc(size_t n_doubles)
+{
+    size_t b = ws_round(n_doubles * sizeof(double) + 8);
+    if (tl_top + b > tl_cap) abort(); /* reservation bug */
+    double *p = (double *)(tl_buf + tl_top);
+    tl_top += b;
+    return p;
+}
+static void ws_free(size_t n_doubles) { tl_top -= ws_round(n_doubles * sizeof(double) + 8); }
+static size_t ws_bound(int64_t n, int64_t L, int64_t S)
+{
+    int64_t nf = n / (S > 0 ? S : 1) + 4;
+    return (size_t)(2 * n + 8 * nf + 4 * L + 64) * sizeof(double) + 64 * 64;
+}
+
+/* ------------------------------------------------------------------------ */
 /* numpy float64 summation                                                  */
 /* ------------------------------------------------------------------------ */
 
@@ -81,7 +112,9 @@ static int cmp_double(const void *pa, const void *pb)
 /* src/feature_extraction.py:46-62 compute_statistics -> mean, std, max, min, median */
 void ora_compute_statistics(const double *seq, int64_t n, double out[5])
 {
-    double *tmp = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    ws_reserve(ws_bound(n, 1, 1));
+    size_t tn = (size_t)(n > 0 ? n : 1);
+    double *tmp = ws_alloc(tn);
     double mean = ora_np_sum(seq, n) / (double)n;
     for (int64_t i = 0; i < n; i++) {
         double d = seq[i] - mean;
@@ -107,7 +140,7 @@ void ora_compute_statistics(const double *seq, int64_t n, double out[5])
     out[2] = mx;
     out[3] = mn;
     out[4] = med;
-    free(tmp);
+    ws_free(tn);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -207,7 +240,9 @@ int64_t ora_endpoint_detection(const double *x, int64_t n, int64_t L, int64_t S,
         return 0;
     }
     int64_t nfr = (n - L) / S + 1; /* :166 */
-    double *scratch = (double *)malloc(sizeof(double) * (size_t)(L > nfr ? L : nfr));
+    ws_reserve(ws_bound(n, L, S));
+    size_t sn = (size_t)(L > nfr ? L : nfr);
+    double *scratch = ws_alloc(sn);
     for (int64_t f = 0; f < nfr; f++) { /* :172-181 */
         E[f] = ora_short_time_energy(x + f * S, L, scratch);
         Z[f] = ora_zero_crossing_rate(x + f * S, L);
@@ -225,7 +260,7 @@ int64_t ora_endpoint_detection(const double *x, int64_t n, int64_t L, int64_t S,
     if (n3 < 0) { /* :207-209 */
         *start = 0;
         *end = n;
-        free(scratch);
+        ws_free(sn);
         return nfr;
     }
     double t2 = noise_e + (speech_e - noise_e) * lo; /* :217 */
@@ -243,7 +278,7 @@ int64_t ora_endpoint_detection(const double *x, int64_t n, int64_t L, int64_t S,
         if (Z[i] <= tz) { n6 = i - 1; break; }
     *start = n1 * S;                                  /* :272 */
     *end = n6 * S + L < n ? n6 * S + L : n;           /* :273 */
-    free(scratch);
+    ws_free(sn);
     return nfr;
 }
 
@@ -266,8 +301,9 @@ int64_t ora_frame_features(const double *x, int64_t n, int64_t L, int64_t S,
                            const double *window, double *E, double *M, double *Z)
 {
     int64_t F = ora_frame_count(n, L, S);
-    double *fr = (double *)malloc(sizeof(double) * (size_t)L);
-    double *scratch = (double *)malloc(sizeof(double) * (size_t)L);
+    ws_reserve(ws_bound(n, L, S));
+    double *fr = ws_alloc((size_t)L);
+    double *scratch = ws_alloc((size_t)L);
     for (int64_t f = 0; f < F; f++) {
         int64_t st = f * S;
         for (int64_t j = 0; j < L; j++) {
@@ -278,8 +314,8 @@ int64_t ora_frame_features(const double *x, int64_t n, int64_t L, int64_t S,
         M[f] = ora_short_time_magnitude(fr, L, scratch);
         Z[f] = ora_zero_crossing_rate(fr, L);
     }
-    free(fr);
-    free(scratch);
+    ws_free((size_t)L);
+    ws_free((size_t)L);
     return F;
 }
 
@@ -301,13 +337,14 @@ static int process_double(double *x, int64_t n, int64_t L, int64_t S, const doub
         int64_t cap = ora_vad_frame_count(n, L, S);
         double *e = vad_e, *z = vad_z;
         double *te = NULL;
+        size_t tn = (size_t)(2 * (cap > 0 ? cap : 1));
         if (!e || !z) {
-            te = (double *)malloc(sizeof(double) * (size_t)(2 * (cap > 0 ? cap : 1)));
+            te = ws_alloc(tn);
             e = te;
             z = te + (cap > 0 ? cap : 1);
         }
         nv = ora_endpoint_detection(x, n, L, S, hi, lo, zr, &st, &en, e, z);
-        free(te);
+        if (te) ws_free(tn);
     }
     if (start_end) {
         start_end[0] = st;
@@ -319,7 +356,7 @@ static int process_double(double *x, int64_t n, int64_t L, int64_t S, const doub
     int64_t F = ora_frame_count(m, L, S);
     if (n_frames) *n_frames = F;
     if (F == 0) return ORA_ERR_NO_FRAMES;
-    double *buf = (double *)malloc(sizeof(double) * (size_t)(3 * F));
+    double *buf = ws_alloc((size_t)(3 * F));
     double *E = buf, *M = buf + F, *Z = buf + 2 * F;
     ora_frame_features(x + st, m, L, S, window, E, M, Z);
     if (feat15) {
@@ -334,7 +371,7 @@ static int process_double(double *x, int64_t n, int64_t L, int64_t S, const doub
             seq[3 * f + 2] = Z[f];
         }
     }
-    free(buf);
+    ws_free((size_t)(3 * F));
     return ORA_OK;
 }
 
@@ -344,11 +381,13 @@ int ora_process_pcm_i16(const int16_t *pcm, int64_t n, int64_t L, int64_t S, con
                         int64_t *n_vad, double *seq, int64_t seq_cap)
 {
     if (L <= 0 || S <= 0) return ORA_ERR_ARGS;
-    double *x = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    ws_reserve(ws_bound(n, L, S));
+    size_t xn = (size_t)(n > 0 ? n : 1);
+    double *x = ws_alloc(xn);
     for (int64_t i = 0; i < n; i++) x[i] = pcm[i] / 32768.0; /* load_wav :35-38 */
     int rc = process_double(x, n, L, S, window, do_vad, hi, lo, zr, feat15, start_end, n_frames,
                             vad_e, vad_z, n_vad, seq, seq_cap);
-    free(x);
+    ws_free(xn);
     return rc;
 }
 
@@ -358,11 +397,13 @@ int ora_process_f64(const double *audio, int64_t n, int64_t L, int64_t S, const 
                     int64_t *n_vad, double *seq, int64_t seq_cap)
 {
     if (L <= 0 || S <= 0) return ORA_ERR_ARGS;
-    double *x = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    ws_reserve(ws_bound(n, L, S));
+    size_t xn = (size_t)(n > 0 ? n : 1);
+    double *x = ws_alloc(xn);
     memcpy(x, audio, sizeof(double) * (size_t)n);
     int rc = process_double(x, n, L, S, window, do_vad, hi, lo, zr, feat15, start_end, n_frames,
                             vad_e, vad_z, n_vad, seq, seq_cap);
-    free(x);
+    ws_free(xn);
     return rc;
 }
 
@@ -399,6 +440,7 @@ int ora_process_batch_i16(const int16_t *pcm, const int64_t *offsets, int64_t B,
 {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > B) nthreads = (int)(B > 0 ? B : 1);
+
     pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
     batch_job *jobs = (batch_job *)malloc(sizeof(batch_job) * (size_t)nthreads);
     for (int t = 0; t < nthreads; t++) {

@@ -118,3 +118,24 @@ def test_too_long_status():
     out = fx(torch.as_tensor(c).cuda(), np.array([0, 44100, 64100]), max_len=30000)
     st = out["status"].cpu().numpy() & 0xFF
     assert st[0] == 4 and st[1] == 0
+
+
+def test_unpadded_buffer_tail():
+    """The packed buffer ends exactly at the last clip (length not a multiple of 8): the partial
+    last 16-B vector is patched in LDS and every sign bit must come from the patched samples."""
+    import torch
+    from src.pipeline import FeatureExtractor, create_window
+    from src.synth import make_clip
+    w = create_window("hamming", 1102)
+    for n, lead, last in ((3000, 5, -300), (2001, 0, -300), (44099, 1, 300), (10000, 3, -300)):
+        c = make_clip(60, n)
+        c[-1] = last
+        pcm = np.concatenate([np.zeros(lead, np.int16), c])
+        off = np.array([0, lead, lead + n], np.int64)
+        for vad in (False, True):
+            fx = FeatureExtractor(1102, 441, "hamming", vad, return_sequences=True)
+            out = {k: v.cpu().numpy() for k, v in fx(torch.as_tensor(pcm).cuda(), off).items()}
+            r = oracle.process_clip(c, 1102, 441, w, do_vad=vad)
+            assert out["n_frames"][1] == r["n_frames"]
+            assert np.array_equal(out["seq"][1, :r["n_frames"], 2], r["seq"][:, 2]), (n, lead, vad)
+            assert not feat_close(out["feat"][1], r["feat"]).any()
