@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--frame-shift", type=int, default=441)
     ap.add_argument("--window", default="hamming")
     ap.add_argument("--no-vad", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="CPU-baseline budget (rank 0, N=1)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
@@ -191,7 +191,7 @@ def cpu_baseline(batch, L, S, window, vad, budget_s):
     rate, dt = run(threads, C)
     reps = 1
     total_frames, total_t = rate * dt, dt
-    while total_t < budget_s and reps < 50:
+    while total_t < budget_s and reps < 5000:
         r2, d2 = run(threads, C)
         total_frames += r2 * d2
         total_t += d2

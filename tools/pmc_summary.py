@@ -3,7 +3,7 @@ import collections, csv, glob, os, sys
 d = sys.argv[1]
 ks = sys.argv[2] if len(sys.argv) > 2 else "extract_kernel"
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
-for f in sorted(glob.glob(os.path.join(d, "p*", "p_counter_collection.csv"))):
+for f in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
     for r in csv.DictReader(open(f)):
         if ks in r["Kernel_Name"]:
             agg[r["Counter_Name"]][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
