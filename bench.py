@@ -108,12 +108,12 @@ def main():
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         elapsed, total_frames, kern_ms = tmax[0].item(), tsum[1].item(), tmax[2].item()
         # the exchange step before KNN (not part of the metric): all-gather of the 15-d vectors
+        from src.distributed import all_gather_rows
         feat = fx(pool[0])["feat"]
-        gathered = [torch.empty_like(feat) for _ in range(world)]
         torch.cuda.synchronize(dev)
         dist.barrier()
         g0 = time.perf_counter()
-        dist.all_gather(gathered, feat)
+        all_gather_rows(feat, total=C * world)
         torch.cuda.synchronize(dev)
         ag_ms = (time.perf_counter() - g0) * 1e3
     else:

@@ -1,0 +1,78 @@
+"""Host-side logic of the drop-in layer: windows, WAV decoding, synthetic data, sharding."""
+import io
+import wave
+
+import numpy as np
+import pytest
+
+
+def test_windows_match_numpy():
+    from src.pipeline import create_window
+    for L in (1, 2, 1024, 1102):
+        assert np.array_equal(create_window("hamming", L), np.hamming(L))
+        assert np.array_equal(create_window("hanning", L), np.hanning(L))
+        assert np.array_equal(create_window("rectangular", L), np.ones(L))
+    with pytest.raises(ValueError):
+        create_window("kaiser", 16)
+
+
+def _wav_bytes(data, width, channels, sr=44100):
+    b = io.BytesIO()
+    with wave.open(b, "wb") as w:
+        w.setnchannels(channels)
+        w.setsampwidth(width)
+        w.setframerate(sr)
+        w.writeframes(data.tobytes())
+    b.seek(0)
+    return b
+
+
+def test_decode_matches_reference_formula():
+    """load_wav (src/audio_processing.py:31-44): 8-bit via uint8 arithmetic (wraps), 16-bit /32768,
+    stereo = channel mean; the integer form times the scale is the float64 audio exactly."""
+    from src.audio_processing import decode_pcm_bytes
+    rng = np.random.default_rng(0)
+    u8 = rng.integers(0, 256, 1000, dtype=np.uint8)
+    a, ints, sc = decode_pcm_bytes(u8.tobytes(), 1, 1)
+    assert np.array_equal(a, (u8 - 128).astype(np.float64) / 128.0)  # numpy uint8 wrap, as the reference
+    assert np.array_equal(ints * sc, a)
+    s16 = rng.integers(-32768, 32768, 2000, dtype=np.int16)
+    a, ints, sc = decode_pcm_bytes(s16.tobytes(), 2, 2)
+    ref = np.mean(s16.astype(np.float64).reshape(-1, 2) / 32768.0, axis=1)
+    assert np.array_equal(a, ref)
+    assert np.array_equal(ints * sc, a)
+    with pytest.raises(ValueError):
+        decode_pcm_bytes(b"\0" * 12, 3, 1)
+
+
+def test_load_wav_pcm_roundtrip(tmp_path):
+    from src.audio_processing import load_wav, load_wav_pcm
+    x = (np.arange(-500, 500) * 31).astype(np.int16)
+    p = tmp_path / "a.wav"
+    p.write_bytes(_wav_bytes(x, 2, 1).read())
+    pcm, sr = load_wav_pcm(str(p))
+    a, sr2 = load_wav(str(p))
+    assert sr == sr2 == 44100 and np.array_equal(pcm, x) and np.array_equal(a, x / 32768.0)
+
+
+def test_synth_is_shardable():
+    from src.synth import make_batch, make_clip
+    full = make_batch(12, base_seed=5)
+    part = make_batch(5, base_seed=5, start=7)
+    assert np.array_equal(full[7:], part)
+    assert np.array_equal(make_clip(5 + 3), full[3])
+    x, y = make_batch(20, with_labels=True)
+    assert np.array_equal(y, np.arange(20) % 10)
+
+
+def test_shard_range_partitions():
+    from src.distributed import shard_range
+    for total in (0, 1, 7, 1000, 100000):
+        for ws in (1, 2, 3, 8):
+            spans = [shard_range(total, r, ws) for r in range(ws)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [h - l for l, h in spans]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard_range(10, 2, 2)
