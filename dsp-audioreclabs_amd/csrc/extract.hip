@@ -1,9 +1,15 @@
 // extract.hip -- fused per-clip feature extraction for gfx950 (CDNA4).
 //
-// Persistent workgroups (1024 threads, one per CU: the clip lives in LDS) walk the batch.  While
-// a workgroup computes clip i out of LDS, the 16-byte loads of clip i+grid are already in flight
-// into registers, so the HBM stream never waits for the compute.  The clip is read from HBM exactly
-// once: algorithmic traffic is 2 B/sample in + 76 B/clip out.
+// Persistent workgroups (512 threads, two per CU) walk the batch, one clip at a time.  The clip is
+// read from HBM once, straight into registers (each thread holds EXTRACT_RREG 32-sample words):
+//   R1  registers: integer sum / min / max + exact per-word moments (sum k, sum k^2) -> LDS
+//   R2  registers: positive-sample bits per word -> LDS (the ZCR of any range is a popcount)
+//   R3  endpoint detection from the per-word summaries (+ the two partial words of each frame,
+//       re-read from L2), p90 by parallel ranks, double-threshold scan
+//   R4  windowed frames of the crop (samples re-read from L2, window (w, w^2) from LDS)
+//   R5  15-d statistics
+// LDS holds only summaries (~36 KB for 1 s), so a second workgroup on the same CU computes while
+// this one waits for HBM.  Algorithmic traffic: 2 B/sample in + 76 B/clip out.
 //
 // Reference functions restated (Hypersonic-cpu/DSP-AudioRecLabs):
 //   preprocess              src/audio_processing.py:78-90
@@ -12,14 +18,14 @@
 //   extract_frame_features  src/feature_extraction.py:12-43
 //   compute_statistics / extract_statistical_features  src/feature_extraction.py:46-88
 //
-// Exactness plan (DESIGN.md §3):
+// Exactness plan (DESIGN.md §2):
 //   * mean / peak: exact integer sums -> mq = fl(K/n), M' = max(fl(kmax-mq), fl(mq-kmin)) are the
 //     reference's float64 values bit for bit (its mean of k/32768 is exact).
 //   * signs and every ZCR: pure integer (sample positive <=> k >= floor(mq)+1): bit-exact.
-//   * endpoint energies: exact int64 moments per frame (sum k, sum k^2) combined with mq in
+//   * endpoint energies: exact integer moments per frame (sum k, sum k^2) combined with mq in
 //     double-double -> relative error ~1e-16; every threshold decision is certified against a
-//     1e-11 margin and, on a near tie, the energies are recomputed in numpy's exact float64 order
-//     (pairwise_sum), so start/end are always the reference's.
+//     1e-11 margin and, on a near tie, the clip is redone with the energies in numpy's exact
+//     float64 order (pairwise_sum), so start/end are always the reference's.
 //   * windowed E/M: fp32 on VALU (tolerance 1e-5 rel., measured ~2e-7); statistics in fp64.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -31,21 +37,22 @@ namespace dsp {
 
 static constexpr int NT = EXTRACT_THREADS;
 static constexpr int NWAVE = NT / 64;
-static constexpr int NR = EXTRACT_MAX_ROUNDS;  // 16-B vectors per thread per clip (max)
-static constexpr int NPF = EXTRACT_PREFETCH;   // of which prefetched into registers
+static constexpr int RREG = EXTRACT_RREG;  // words per thread in registers
+static constexpr int NRV = 4 * RREG;       // 16-B vectors per thread in registers
 
 #ifdef DSP_STAMPS
-// diagnostic build only (make stamps): per-phase shader-clock stamps of each clip
-__device__ unsigned long long *g_stamps;
-__device__ uint32_t *g_dump;  // chg words of each clip after R2a (4096 words per clip)
+// diagnostic build only (make stamps): per-phase shader-clock stamps of each clip.  The buffer
+// pointer is a kernel argument (SGPRs), so a stamp never waits on a memory load.
 #define STAMP(clip, k)                                                                           \
     do {                                                                                         \
-        if (threadIdx.x == 0 && g_stamps) g_stamps[(size_t)(clip) * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+        if (threadIdx.x == 0 && p.stamps) p.stamps[(size_t)(clip) * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+#define SKIP(bit) ((p.skip & (bit)) != 0)  // phase ablation for timing (outputs are garbage)
 #else
 #define STAMP(clip, k) \
     do {               \
     } while (0)
+#define SKIP(bit) false
 #endif
 
 struct ExtractParams {
@@ -62,10 +69,14 @@ struct ExtractParams {
     int ld_vad;
     float *seq;
     int ld_seq;
+    unsigned long long *stamps;  // diagnostic build only (else null)
+    int skip;                    // diagnostic build only: phases to skip (timing ablation)
 };
 
 typedef short short8 __attribute__((ext_vector_type(8)));
-
+template <bool B> struct BoolT {
+    static constexpr bool value = B;
+};
 typedef short short2v __attribute__((ext_vector_type(2)));
 
 // ---- wave reductions on DPP (VALU lane permutes, no LDS crossbar) + 4 readlanes -------------
@@ -288,36 +299,21 @@ __device__ double np_lerp(double a, double b, double g)
 
 // ------------------------------------------------------------------------------------------
 struct Shared {
-    int red_s[NWAVE], red_a[NWAVE], red_b[NWAVE];
+    long long red_k[NWAVE];
+    int red_a[NWAVE], red_b[NWAVE];
     double pa, pb;            // the two order statistics of the VAD energies around p90
     double oslo[3], oshi[3];  // order statistics (F-1)/2 and F/2 of E, M, ZCR (medians)
-    double noise_buf[16];
     int n3, n1, n6, exact, j0, j1, ndefer;
 };
 static_assert(sizeof(Shared) <= EXTRACT_SHARED_BYTES, "grow EXTRACT_SHARED_BYTES");
 
-// set change-bits in buffer-bit range [x0, x1) (bit u = sign change between samples u, u+1)
-__device__ __forceinline__ int popc_range(const uint32_t *chg, int x0, int x1)
-{
-    if (x1 <= x0) return 0;
-    const int w0 = x0 >> 5, w1 = (x1 - 1) >> 5;
-    int c = 0;
-    for (int w = w0; w <= w1; w++) {
-        uint32_t m = chg[w];
-        if (w == w0) m &= ~0u << (x0 & 31);
-        if (w == w1 && ((x1 & 31) != 0)) m &= (1u << (x1 & 31)) - 1u;
-        c += __popc(m);
-    }
-    return c;
-}
-
 struct ClipRef {
     int64_t base;  // 8-aligned first sample index of the clip's vectors
-    int lead, n, nvec, lim;
+    int lead, n, nvec, nword;
     bool ok;
 };
 
-__device__ __forceinline__ ClipRef clip_ref(const ExtractParams &p, int i, int64_t total)
+__device__ __forceinline__ ClipRef clip_ref(const ExtractParams &p, int i)
 {
     ClipRef c;
     const int64_t o0 = p.offsets[i], nn = p.offsets[i + 1] - o0;
@@ -326,48 +322,41 @@ __device__ __forceinline__ ClipRef clip_ref(const ExtractParams &p, int i, int64
     c.base = o0 & ~(int64_t)7;
     c.lead = (int)(o0 - c.base);
     c.nvec = (c.lead + c.n + 7) >> 3;
-    c.lim = c.ok ? (int)min((int64_t)c.nvec, (total - c.base) >> 3) : 0;
+    c.nword = (c.lead + c.n + 31) >> 5;
     return c;
 }
 
-// 16-B loads of rounds [R0, R1) of a clip (unconditional, clamped addresses: no per-load branch,
-// so no vmcnt(0) between them).  The prefetch of the next clip is issued in slices spread over the
-// phases of the current one, so the issue never blocks on a full memory queue.
-template <int R0, int R1>
-__device__ __forceinline__ void issue_rounds(short8 (&regs)[NPF], const int16_t *pcm, const ClipRef &c,
-                                             int tid)
-{
-    if (c.lim <= 0) return;
-    const short8 *src = reinterpret_cast<const short8 *>(pcm + c.base);
-#pragma unroll
-    for (int r = R0; r < R1; r++) regs[r] = __builtin_nontemporal_load(src + min(tid + r * NT, c.lim - 1));
-}
-__device__ __forceinline__ void issue_loads(short8 (&regs)[NPF], const int16_t *pcm, const ClipRef &c,
-                                            int tid)
-{
-    issue_rounds<0, NPF>(regs, pcm, c, tid);
-}
-static_assert(NPF % 4 == 0, "prefetch issued in four slices");
-#define PREFETCH_SLICE(k)                                                                     \
-    do {                                                                                      \
-        if (!EXACT && prefetch) issue_rounds<(k) * (NPF / 4), ((k) + 1) * (NPF / 4)>(regs, p.pcm, nxt, tid); \
-    } while (0)
-
 struct Ctx {
     Shared *sh;
-    int16_t *buf;  // clip samples, buffer coordinates u = i + lead
-    uint32_t *chg;
-    uint32_t *pos;                     // positive-sample bits
-    int *sgS, *sgZ;                    // per-segment sum k, sign changes
-    unsigned long long *sgQ;           // per-segment sum k^2
-    float2 *wtab;                      // (window, window^2)
+    const float *wtab;  // EXTRACT_WROW(L) floats per shifted copy r = 0..3 (extract_layout.h)
+    uint32_t *posw;      // bit u of the buffer: sample u is real and positive after preprocess
+    unsigned long long *wS2;
+    int *wS1;
     double *vE;
     int32_t *vZ;
     float *fE, *fM;
     int32_t *fZ;
+    int *rank;  // rank scratch: nvcap or 3 * fcap ints
     int *defer;
     int64_t total;
+    int stamp_clip;  // clip index for the diagnostic stamps
 };
+
+// 16-B vectors of the clip buffer.  The buffer's last vector may reach up to 15 bytes past
+// offsets[B]; pcm is 16-B aligned, so such a vector never crosses a page and the read cannot
+// fault.  Bytes outside a clip are masked by every consumer ([lead, lead + n) ranges, zero window
+// weights), so no element-wise patching is needed.
+__device__ __forceinline__ short8 load_vec(const ExtractParams &p, const ClipRef &c, int v)
+{
+    return reinterpret_cast<const short8 *>(p.pcm + c.base)[v];
+}
+// the four 16-B loads of word w (unconditional, clamped to the clip's last vector)
+__device__ __forceinline__ void issue_word(short8 *q, const ExtractParams &p, const ClipRef &c, int w)
+{
+    const short8 *src = reinterpret_cast<const short8 *>(p.pcm + c.base);
+#pragma unroll
+    for (int k = 0; k < 4; k++) q[k] = src[min(4 * w + k, c.nvec - 1)];
+}
 
 __device__ __forceinline__ short2v half_pair(const short8 &x, int i)
 {
@@ -379,29 +368,28 @@ __device__ __forceinline__ short2v half_pair(const short8 &x, int i)
     }
 }
 
-// exact moments of 8 samples: sum k (packed dot with ones) and sum k^2 (packed dot of each pair,
-// <= 2^31 read as unsigned, accumulated in 64 bits)
-__device__ __forceinline__ void moments8(const short8 &x, int &s1, unsigned long long &s2)
+// sign-change bits of buffer word w: bit b <-> (pos(32w+b) != pos(32w+b+1))
+__device__ __forceinline__ uint32_t chg_word(const uint32_t *posw, int w)
 {
-    const short2v ones = {1, 1};
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const short2v d = half_pair(x, i);
-        s1 = __builtin_amdgcn_sdot2(d, ones, s1, false);
-        s2 += (unsigned)__builtin_amdgcn_sdot2(d, d, 0, false);
-    }
+    const uint32_t a = posw[w], b = posw[w + 1];
+    return a ^ ((a >> 1) | (b << 31));
 }
-__device__ __forceinline__ unsigned long long dpp_quad_sum64(unsigned long long v)
+// set change bits in buffer-bit range [x0, x1), words split over `nl` lanes starting at `l0`
+__device__ __forceinline__ int chg_count(const uint32_t *posw, int x0, int x1, int l0, int nl)
 {
-    const auto add = [](unsigned long long a, unsigned long long b) { return a + b; };
-#pragma unroll
-    for (int s = 0; s < 2; s++) {
-        const int ctl = s == 0 ? DPP_QXOR1 : DPP_QXOR2;
-        const unsigned lo = dpp_i((int)(unsigned)v, ctl), hi = dpp_i((int)(unsigned)(v >> 32), ctl);
-        v = add(v, ((unsigned long long)hi << 32) | lo);
+    int c = 0;
+    if (x1 > x0) {
+        const int w0 = x0 >> 5, w1 = (x1 - 1) >> 5;
+        for (int w = w0 + l0; w <= w1; w += nl) {
+            uint32_t m = chg_word(posw, w);
+            if (w == w0) m &= ~0u << (x0 & 31);
+            if (w == w1 && (x1 & 31)) m &= (1u << (x1 & 31)) - 1u;
+            c += __popc(m);
+        }
     }
-    return v;
+    return c;
 }
+__device__ __forceinline__ int pos_bit(const uint32_t *posw, int u) { return (posw[u >> 5] >> (u & 31)) & 1; }
 
 // ---- 256-frame bit sets (wave-uniform: four ballots) ------------------------------------------
 struct Bits256 {
@@ -476,6 +464,7 @@ __device__ __forceinline__ int vad_scan(const ExtractParams &p, const Ctx &c, in
         t2 = noise_e + (p90 - noise_e) * p.lo;  // :217
         tz = noise_z * p.zr;                    // :247
     }
+    STAMP(c.stamp_clip, 10);
     auto near = [&](double e, double t) {
         const double d = fabs(e - t);
         return d <= 1e-11 * fmax(fabs(e), fabs(t)) && !(e == 0.0 && t == 0.0);
@@ -576,95 +565,161 @@ __device__ __forceinline__ int vad_scan(const ExtractParams &p, const Ctx &c, in
         sh->n1 = n1;
         sh->n6 = n6;
     }
+    STAMP(c.stamp_clip, 11);
     return flag;
 }
 
-// rank (ties by index) of every element of v[0..n) -> the elements of ranks r0 / r1 (all threads)
-template <typename T>
-__device__ __forceinline__ void rank_select(const T *v, int n, int r0, int r1, double *o0, double *o1,
-                                            int tid)
+// Ranks (ties broken by index) of nseq sequences of n elements, element (q, i) = get(q, i).  Wave w
+// compares every element with its chunk of the other elements; the partial counts are combined
+// with integer LDS atomics (exact, order-free).  rk[nseq * n] must be zeroed before the barrier
+// that precedes this call; the ranks are complete after the next barrier.
+template <typename Get>
+__device__ __forceinline__ void rank_partial(Get get, int nseq, int n, int *rk, int wid, int lane)
 {
-    for (int i = tid; i < n; i += NT) {
-        const T e = v[i];
-        int r = 0;
-#pragma unroll 8
-        for (int j = 0; j < n; j++) {
-            const T o = v[j];
-            r += (o < e) || (o == e && j < i);
+    const int per = (n + NWAVE - 1) / NWAVE;
+    const int jlo = wid * per, jhi = min(n, jlo + per);
+    if (jlo >= jhi) return;
+    for (int q = 0; q < nseq; q++)
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + lane;
+            const auto e = get(q, i < n ? i : 0);
+            int r = 0;
+#pragma unroll 4
+            for (int j = jlo; j < jhi; j++) {
+                const auto o = get(q, j);
+                r += (o < e) || (o == e && j < i);
+            }
+            if (i < n && r) atomicAdd(&rk[q * n + i], r);
         }
-        if (r == r0) *o0 = (double)e;
-        if (r == r1) *o1 = (double)e;
+}
+
+
+__device__ __forceinline__ unsigned long long dpp_quad_sum64(unsigned long long v)
+{
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        const int ctl = s == 0 ? DPP_QXOR1 : DPP_QXOR2;
+        const unsigned lo = dpp_i((int)(unsigned)v, ctl), hi = dpp_i((int)(unsigned)(v >> 32), ctl);
+        v += ((unsigned long long)hi << 32) | lo;
+    }
+    return v;
+}
+__device__ __forceinline__ long long dpp_quad_sum_i64(long long v)
+{
+    return (long long)dpp_quad_sum64((unsigned long long)v);
+}
+
+// Order statistics r0 / r1 (ranks with ties broken by index) of v[0..n), n <= 256: every wave
+// holds the whole sequence in registers (lane + 64k), wave w ranks elements w, w + NWAVE, ...
+// with one ballot per chunk.  Lane 0 of the wave that finds them stores them.
+template <typename T, typename Get>
+__device__ __forceinline__ void ballot_select(Get get, int n, int r0, int r1, double *o0, double *o1,
+                                              int wid, int lane)
+{
+    T x[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int j = lane + 64 * k;
+        x[k] = j < n ? get(j) : (T)0;
+    }
+    const int kc = (n + 63) >> 6;
+    for (int i = wid; i < n; i += NWAVE) {
+        const T e = get(i);
+        int r = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (k < kc) {
+                const int j = lane + 64 * k;
+                r += __popcll(__ballot(j < n && (x[k] < e || (x[k] == e && j < i))));
+            }
+        }
+        if (lane == 0) {
+            if (r == r0) *o0 = (double)e;
+            if (r == r1) *o1 = (double)e;
+        }
     }
 }
 
-// One clip, start to finish.  EXACT = false: the streaming path (registers prefetched, endpoint
-// energies from exact moments, decisions certified); returns false when a decision is a near tie
-// (the clip is then redone with EXACT = true after the persistent loop).
+// One clip, start to finish; its first RREG words are already in flight into regs (word
+// r * NT + tid in regs[4r .. 4r+3]).  EXACT = false: endpoint energies from exact moments,
+// decisions certified; returns false on a near tie (the clip is then redone with EXACT = true
+// after the persistent loop).
 template <bool EXACT>
-__device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, int i,
-                                          const ClipRef &cur, short8 (&regs)[NPF], bool prefetch,
-                                          const ClipRef &nxt)
+__device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, int i, const ClipRef &cur,
+                                          short8 (&regs)[NRV])
 {
     Shared *sh = c.sh;
-    int16_t *buf = c.buf;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int L = p.L, S = p.S;
-    const int n = cur.n, lead = cur.lead, nvec = cur.nvec;
-    const int16_t *cl = buf + lead;  // cl[i], sample coords
-    const int64_t total = c.total;
+    const int n = cur.n, lead = cur.lead, nword = cur.nword;
     float *featb = p.feat + (size_t)i * 15;
+    const int16_t *clip_g = p.pcm + cur.base + lead;  // the clip in global memory, sample coords
     STAMP(i, 0);
 
-    // ---- R1: clip -> LDS; integer sum / min / max (packed 16-bit) ---------------------------
-    int s1 = 0, kmin_s = 0x7fffffff, kmax_s = -0x7fffffff - 1;
+    // ---- R1: integer sum / min / max; exact moments per 32-sample word -----------------------
+    long long K = 0;
+    int kmin_s = 0x7fffffff, kmax_s = -0x7fffffff - 1;
     short2v pmin = {32767, 32767}, pmax = {-32768, -32768};
-    auto consume = [&](short8 val, int v) {
-        if (v >= cur.lim && v < nvec) {  // last vector of the pcm buffer: partial
-            const int16_t *src = p.pcm + cur.base + 8 * v;
-            for (int e = 0; e < 8; e++) val[e] = (cur.base + 8 * v + e < total) ? src[e] : 0;
-        }
-        if (v < nvec) {
-            *reinterpret_cast<short8 *>(buf + 8 * v) = val;
-            const int u0 = 8 * v;
-            if (u0 >= lead && u0 + 8 <= lead + n) {
-                const short2v ones = {1, 1};
+    auto r1_word = [&](const short8 *q, int w) {
+        int s1 = 0;
+        unsigned long long s2 = 0;
+        if (w > 0 && w < nword - 1) {  // all 32 samples are the clip's
+            const short2v ones = {1, 1};
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const short2v d = half_pair(val, q);
+            for (int k = 0; k < 4; k++)
+#pragma unroll
+                for (int h = 0; h < 4; h++) {
+                    const short2v d = half_pair(q[k], h);
                     pmin = __builtin_elementwise_min(pmin, d);
                     pmax = __builtin_elementwise_max(pmax, d);
                     s1 = __builtin_amdgcn_sdot2(d, ones, s1, false);
+                    s2 += (unsigned)__builtin_amdgcn_sdot2(d, d, 0, false);  // <= 2^31: unsigned
                 }
-            } else {  // first / last vector of the clip
+        } else {  // first / last word of the clip: real samples only
+#pragma unroll 1
+            for (int k = 0; k < 4; k++) {
+                const short8 v = k == 0 ? q[0] : k == 1 ? q[1] : k == 2 ? q[2] : q[3];
+#pragma unroll
                 for (int e = 0; e < 8; e++) {
-                    const int u = u0 + e;
+                    const int u = 32 * w + 8 * k + e;
+                    const int x = v[e];
                     if (u >= lead && u < lead + n) {
-                        const int k = val[e];
-                        s1 += k;
-                        kmin_s = min(kmin_s, k);
-                        kmax_s = max(kmax_s, k);
+                        s1 += x;
+                        s2 += (unsigned)(x * x);
+                        kmin_s = min(kmin_s, x);
+                        kmax_s = max(kmax_s, x);
                     }
                 }
             }
         }
+        c.wS1[w] = s1;
+        c.wS2[w] = s2;
+        K += s1;
     };
-    const short8 *gsrc = reinterpret_cast<const short8 *>(p.pcm + cur.base);
-    if (!EXACT) {
+    // clips of up to RREG * NT words stream from the registers loaded before this call; longer
+    // ones are read word by word here and again in R2 (the second read hits L2)
+    const bool inreg = nword <= RREG * NT;
+    if (inreg) {
 #pragma unroll
-        for (int r = 0; r < NPF; r++) consume(regs[r], tid + r * NT);
-    }
+        for (int r = 0; r < RREG; r++) {
+            const int w = r * NT + tid;
+            if (w < nword && !SKIP(128)) r1_word(&regs[4 * r], w);
+        }
+    } else {
 #pragma unroll 1
-    for (int v = tid + (EXACT ? 0 : NPF * NT); v - tid < nvec; v += NT) {  // long clips / exact redo
-        short8 val = {};
-        if (v < cur.lim) val = gsrc[v];
-        consume(val, v);
+        for (int w = tid; w < nword; w += NT) {
+            short8 q[4];
+            issue_word(q, p, cur, w);
+            r1_word(q, w);
+        }
     }
     {
         const int kmn = min(kmin_s, min((int)pmin.x, (int)pmin.y));
         const int kmx = max(kmax_s, max((int)pmax.x, (int)pmax.y));
-        const int ws = wave_sum(s1), wmn = wave_min(kmn), wmx = wave_max(kmx);
+        const long long ks = wave_sum(K);
+        const int wmn = wave_min(kmn), wmx = wave_max(kmx);
         if (lane == 0) {
-            sh->red_s[wid] = ws;
+            sh->red_k[wid] = ks;
             sh->red_a[wid] = wmn;
             sh->red_b[wid] = wmx;
         }
@@ -673,15 +728,15 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     // remove_dc / normalize_audio (:49-75) in sample units, computed redundantly by every thread:
     // the reference's float64 mean of k/32768 is exact, so m = fl(K/n) and the peak is
     // max(fl(kmax - m), fl(m - kmin)); a sample is positive after preprocess <=> k >= t.
-    long long K = 0;
+    long long Kt = 0;
     int kmin = 0x7fffffff, kmax = -0x7fffffff - 1;
 #pragma unroll
     for (int w = 0; w < NWAVE; w++) {
-        K += sh->red_s[w];
+        Kt += sh->red_k[w];
         kmin = min(kmin, sh->red_a[w]);
         kmax = max(kmax, sh->red_b[w]);
     }
-    const double mq = (double)K / (double)n;
+    const double mq = (double)Kt / (double)n;
     const double Mp = fmax((double)kmax - mq, mq - (double)kmin);
     const int tpos = (int)floor(mq) + 1;
     const int t0 = (int)floor(mq + 0.5);
@@ -690,164 +745,116 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     const int nv = (p.do_vad && n >= L) ? (n - L) / S + 1 : 0;
     STAMP(i, 1);
 
-    // ---- R2a: positive-sample bits (pos byte v = buffer samples 8v..8v+7; pos(u): sample u is
-    //      real and positive after preprocess), then sign-change bits at word level:
-    //      chg bit u = pos(u) ^ pos(u+1) for real pairs ---------------------------------------
-    unsigned char *posb = reinterpret_cast<unsigned char *>(c.pos);
+    // ---- R2: positive-sample bits, one 32-bit word per 32 buffer samples ---------------------
     const bool tbig = tpos > 32767;  // no int16 sample can be positive
     const short2v tt = {(short)(tbig ? 32767 : tpos), (short)(tbig ? 32767 : tpos)};
-    auto pos_of = [&](const short8 &val, int v) {
-        if (v >= nvec) return;
-        unsigned P = 0u;
-        if (!tbig) {
-            const unsigned a0 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 0), tt));
-            const unsigned a1 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 1), tt));
-            const unsigned a2 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 2), tt));
-            const unsigned a3 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 3), tt));
-            // the four sign bytes of each pair of dwords, then their top bits (k < t)
-            const unsigned x01 = __builtin_amdgcn_perm(a1, a0, 0x07050301u) & 0x80808080u;
-            const unsigned x23 = __builtin_amdgcn_perm(a3, a2, 0x07050301u) & 0x80808080u;
-            P = ~(((x01 * 0x00204081u) >> 28) | (((x23 * 0x00204081u) >> 28) << 4)) & 0xFFu;
-        }
-        const int u0 = 8 * v;
-        if (u0 < lead || u0 + 8 > lead + n) {  // first / last vector: real samples only
-            const int lo_ = min(max(lead - u0, 0), 8), hi_ = min(max(lead + n - u0, 0), 8);
-            P &= ((1u << hi_) - 1u) & ~((1u << lo_) - 1u);
-        }
-        posb[v] = (unsigned char)P;
+    auto pos_byte = [&](const short8 &val) -> uint32_t {
+        if (tbig) return 0u;
+        const unsigned a0 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 0), tt));
+        const unsigned a1 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 1), tt));
+        const unsigned a2 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 2), tt));
+        const unsigned a3 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 3), tt));
+        // the sign bytes of the four 16-bit results of each dword pair, then their top bits (k < t)
+        const unsigned x01 = __builtin_amdgcn_perm(a1, a0, 0x07050301u) & 0x80808080u;
+        const unsigned x23 = __builtin_amdgcn_perm(a3, a2, 0x07050301u) & 0x80808080u;
+        return ~(((x01 * 0x00204081u) >> 28) | (((x23 * 0x00204081u) >> 28) << 4)) & 0xFFu;
     };
-    const short8 *bv = reinterpret_cast<const short8 *>(buf);
-    if (!EXACT) {
-#pragma unroll
-        for (int r = 0; r < NPF; r++) {  // the buffer's partial last vector was patched in LDS only
-            const int v = tid + r * NT;
-            pos_of(v < cur.lim ? regs[r] : bv[min(v, nvec)], v);
+    auto r2_word = [&](const short8 *q, int w) {
+        uint32_t P = pos_byte(q[0]) | (pos_byte(q[1]) << 8) | (pos_byte(q[2]) << 16) | (pos_byte(q[3]) << 24);
+        if (w == 0 || w == nword - 1) {  // real samples only
+            const int lo_ = min(max(lead - 32 * w, 0), 32), hi_ = min(max(lead + n - 32 * w, 0), 32);
+            const uint32_t mhi = hi_ >= 32 ? ~0u : ((1u << hi_) - 1u);
+            const uint32_t mlo = lo_ >= 32 ? 0u : ~((1u << lo_) - 1u);
+            P &= mhi & mlo;
         }
-    }
+        c.posw[w] = P;
+    };
+    if (inreg) {
+#pragma unroll
+        for (int r = 0; r < RREG; r++) {
+            const int w = r * NT + tid;
+            if (w < nword && !SKIP(64)) r2_word(&regs[4 * r], w);
+        }
+    } else {
 #pragma unroll 1
-    for (int v = tid + (EXACT ? 0 : NPF * NT); v - tid < nvec; v += NT) pos_of(v < nvec ? bv[v] : short8{}, v);
-    if (tid < 8) posb[nvec + tid] = 0;
-    PREFETCH_SLICE(0);
-    __syncthreads();
-    {
-        // in place: every thread reads its words (and the next word's first bit), then, after a
-        // barrier, writes the change bits over them
-        const int nw = (nvec + 3) >> 2;
-        const int rlo = lead, rhi = lead + n - 1;  // real pairs start in [rlo, rhi)
-        constexpr int MW = (EXTRACT_MAX_ROUNDS * NT * 8 / 32 + NT - 1) / NT;  // words per thread
-        uint32_t chw[MW];
-#pragma unroll
-        for (int k = 0; k < MW; k++) {
-            const int w = tid + k * NT;
-            uint32_t ch = 0;
-            if (w < nw) {
-                const uint32_t p0 = c.pos[w], p1 = c.pos[w + 1];
-                ch = p0 ^ ((p0 >> 1) | (p1 << 31));
-                const int b0 = 32 * w;
-                if (b0 < rlo || b0 + 32 > rhi) {
-                    const int lo_ = min(max(rlo - b0, 0), 32), hi_ = min(max(rhi - b0, 0), 32);
-                    const uint32_t mhi = hi_ >= 32 ? ~0u : ((1u << hi_) - 1u);
-                    const uint32_t mlo = lo_ >= 32 ? 0u : ~((1u << lo_) - 1u);
-                    ch &= mhi & mlo;
-                }
-            }
-            chw[k] = ch;
+        for (int w = tid; w < nword; w += NT) {
+            short8 q[4];
+            issue_word(q, p, cur, w);
+            r2_word(q, w);
         }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < MW; k++) {
-            const int w = tid + k * NT;
-            if (w < nw) c.chg[w] = chw[k];
-        }
-        if (tid < 2) c.chg[nw + tid] = 0;
     }
+    if (tid < 2) c.posw[nword + tid] = 0;
     __syncthreads();
-#ifdef DSP_STAMPS
-    if (g_dump)
-        for (int w = tid; w < 4096; w += NT) g_dump[(size_t)i * 4096 + w] = w < (nvec + 3) / 4 + 2 ? c.chg[w] : 0xdeadbeefu;
-#endif
     STAMP(i, 2);
-
-    // ---- R2b: exact moments + sign changes per segment [qS, qS+r), [qS+r, (q+1)S), L = aS + r:
-    //      frame f = segments of hops f..f+a-1 + the head segment of hop f+a ------------------
-    const int a_ = L / S, r_ = L % S;
-    if (!EXACT && nv > 0) {
-        const int nseg = 2 * (nv + a_);
-        const int jj = tid & 3;
-        for (int sg = tid >> 2; sg < nseg; sg += NT / 4) {
-            const int q = sg >> 1, h = sg & 1;
-            int lo, hi;
-            if (r_ > 0) {
-                lo = q * S + (h ? r_ : 0);
-                hi = h ? (q + 1) * S : q * S + r_;
-            } else {
-                lo = q * S;
-                hi = h ? lo : (q + 1) * S;
-            }
-            hi = min(hi, n);
-            lo = min(lo, hi);
-            const int ulo = lo + lead, uhi = hi + lead;
-            int a1 = 0, zc = 0;
-            unsigned long long q2 = 0;
-            if (uhi > ulo) {
-                for (int v = (ulo >> 3) + jj; v <= ((uhi - 1) >> 3); v += 4) {
-                    short8 x = bv[v];
-                    const int u0 = 8 * v;
-                    const int mlo = max(ulo - u0, 0), mhi = min(uhi - u0, 8);
-                    if (mlo > 0 || mhi < 8)
-                        for (int e = 0; e < 8; e++)
-                            if (e < mlo || e >= mhi) x[e] = 0;
-                    moments8(x, a1, q2);
-                }
-                const int w0 = ulo >> 5, w1 = (uhi - 1) >> 5;
-                for (int w = w0 + jj; w <= w1; w += 4) {
-                    uint32_t m = c.chg[w];
-                    if (w == w0) m &= ~0u << (ulo & 31);
-                    if (w == w1 && (uhi & 31)) m &= (1u << (uhi & 31)) - 1u;
-                    zc += __popc(m);
-                }
-            }
-            a1 = dpp_quad_reduce(a1, OpAdd());
-            q2 = dpp_quad_sum64(q2);
-            zc = dpp_quad_reduce(zc, OpAdd());
-            if (jj == 0) {
-                c.sgS[sg] = a1;
-                c.sgQ[sg] = q2;
-                c.sgZ[sg] = zc;
-            }
-        }
-        __syncthreads();
-        STAMP(i, 7);
-    }
-
-    PREFETCH_SLICE(1);
 
     // ---- R3: endpoint detection (:161-273) ------------------------------------------------
     int st = 0, en = n;
     if (nv > 0) {
-        for (int f = tid; f < nv; f += NT) {
-            const int ua = lead + f * S;  // buffer coords of the frame start
-            if (EXACT) {
-                c.vE[f] = np_energy_exact(cl, f * S, L, mq, Mp);
-                c.vZ[f] = popc_range(c.chg, ua, ua + L - 1);
-            } else {
-                long long S1 = 0;
-                unsigned long long S2 = 0;
-                int zc = 0;
-                auto add = [&](int sg) {
-                    S1 += c.sgS[sg];
-                    S2 += c.sgQ[sg];
-                    zc += c.sgZ[sg];
-                };
-                for (int q = f; q < f + a_; q++) {
-                    add(2 * q);
-                    if (r_ > 0) add(2 * q + 1);
+        // frame f = buffer samples [u0, u0 + L): exact moments from the word sums plus the two
+        // partial words (re-read from L2), sign changes from the bits; one quad per frame
+        const int q4 = tid >> 2, lq = tid & 3;
+        for (int f0 = 0; f0 < nv; f0 += NT / 4) {
+            const int f = f0 + q4;
+            const bool act = f < nv;
+            long long s1 = 0;
+            unsigned long long s2 = 0;
+            int zc = 0;
+            if (act && !SKIP(1)) {
+                const int u0 = lead + f * S, u1 = u0 + L;
+                if (!EXACT) {
+                    const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
+                    // the partial words at the frame's ends: lane 0 the first, lane 1 the last;
+                    // their loads go out before the LDS sums so the L2 latency overlaps them
+                    int pw = -1, e0 = 0, e1 = 0;
+                    if (lq == 0 && (u0 & 31)) {
+                        pw = wa;
+                        e0 = u0 & 31;
+                        e1 = min(32, u1 - 32 * wa);
+                    } else if (lq == 1 && (u1 & 31) && (wb != wa || !(u0 & 31))) {
+                        pw = wb;
+                        e0 = max(0, u0 - 32 * wb);
+                        e1 = u1 & 31;
+                    }
+                    short8 q[4];
+                    const int lw = pw >= 0 ? pw : wa;
+#pragma unroll
+                    for (int k = 0; k < 4; k++) q[k] = load_vec(p, cur, min(4 * lw + k, cur.nvec - 1));
+                    const int wi0 = (u0 & 31) ? wa + 1 : wa, wi1 = (u1 & 31) ? wb - 1 : wb;
+#pragma unroll 3
+                    for (int w = wi0 + lq; w <= wi1; w += 4) {
+                        s1 += c.wS1[w];
+                        s2 += c.wS2[w];
+                    }
+                    if (pw >= 0) {
+                        int t1 = 0;
+                        unsigned long long t2 = 0;
+#pragma unroll 1
+                        for (int k = 0; k < 4; k++) {
+                            const short8 v = k == 0 ? q[0] : k == 1 ? q[1] : k == 2 ? q[2] : q[3];
+#pragma unroll
+                            for (int e = 0; e < 8; e++) {
+                                const int x = v[e];
+                                const int ee = 8 * k + e;
+                                if (ee >= e0 && ee < e1) {
+                                    t1 += x;
+                                    t2 += (unsigned)(x * x);
+                                }
+                            }
+                        }
+                        s1 += t1;
+                        s2 += t2;
+                    }
                 }
-                if (r_ > 0) add(2 * (f + a_));
-                c.vE[f] = energy_from_moments(S2, S1, L, mq, Mp);
-                // the last segment also counted the pair leaving the frame
-                const int ub = ua + L - 1;
-                c.vZ[f] = zc - (int)((c.chg[ub >> 5] >> (ub & 31)) & 1u);
+                zc = chg_count(c.posw, u0, u1 - 1, lq, 4);
+            }
+            s1 = dpp_quad_sum_i64(s1);
+            s2 = dpp_quad_sum64(s2);
+            zc = dpp_quad_reduce(zc, OpAdd());
+            if (act && lq == 0) {
+                c.rank[f] = 0;
+                c.vE[f] = EXACT ? np_energy_exact(clip_g, f * S, L, mq, Mp)
+                                : energy_from_moments(s2, s1, L, mq, Mp);
+                c.vZ[f] = zc;
             }
         }
         __syncthreads();
@@ -862,18 +869,35 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                 r0 = (int)floor(vi);
                 r1 = r0 + 1;
             }
-            rank_select<double>(c.vE, nv, r0, r1, &sh->pa, &sh->pb, tid);
+            if (SKIP(2)) {
+                if (tid == 0) sh->pa = sh->pb = c.vE[r0];
+            } else if (nv <= 256) {
+                ballot_select<double>([&](int j) { return c.vE[j]; }, nv, r0, r1, &sh->pa, &sh->pb, wid, lane);
+            } else {  // long clips: partial ranks over all waves
+                rank_partial([&](int, int j) { return c.vE[j]; }, 1, nv, c.rank, wid, lane);
+                __syncthreads();
+                for (int f = tid; f < nv; f += NT) {
+                    const int r = c.rank[f];
+                    if (r == r0) sh->pa = c.vE[f];
+                    if (r == r1) sh->pb = c.vE[f];
+                }
+            }
         }
         __syncthreads();
         STAMP(i, 3);
-        if (wid == 0) {
+        if (SKIP(4)) {
+            if (tid == 0) {
+                sh->n3 = 0;
+                sh->n1 = min(30, nv - 1);
+                sh->n6 = min(55, nv - 1);
+                sh->exact = 0;
+            }
+        } else if (wid == 0) {
             const int flag = vad_scan<!EXACT>(p, c, nv, lane);
             if (lane == 0) sh->exact = (!EXACT && Mp > 0.0) ? flag : 0;
         }
         __syncthreads();
         if (!EXACT && sh->exact) {  // near tie: redo in numpy's exact order after the loop
-            PREFETCH_SLICE(2);
-            PREFETCH_SLICE(3);
             return false;
         }
         if (sh->n3 >= 0) {
@@ -886,127 +910,129 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                 p.vad_zcr[(size_t)i * p.ld_vad + f] = c.vZ[f];
             }
     }
-    PREFETCH_SLICE(2);
     STAMP(i, 4);
 
     // ---- R4: windowed frames over the crop [st, en) (:378, :299-333; fe.py:12-43) ---------
+    // wave per frame; the frame's 16-B vectors are re-read from L2 (lane -> vectors va + lane +
+    // 64k); E = sum w^2 x^2, M = sum w |x| with x = (k - t0) - delta, scaled by 1/M' at the end.
     const int m = en - st;  // > 0 always (start < end)
     const int F = (m <= L) ? 1 : (m - L + S - 1) / S + 1;
     const int j0 = sh->j0, j1 = sh->j1;
-    const float2 *wtab = c.wtab;
-    auto zcr_words = [&](int fs) {  // this lane's share of the frame's sign changes
-        const int ia = fs + j0, ib = min(fs + j1, en - 1);
-        int cnt = 0;
-        if (ia < ib) {
-            const int x0 = ia + lead, x1 = ib + lead;
-            const int w0 = x0 >> 5, w1 = (x1 - 1) >> 5;
-            for (int w = w0 + lane; w <= w1; w += 64) {
-                uint32_t mm = c.chg[w];
-                if (w == w0) mm &= ~0u << (x0 & 31);
-                if (w == w1 && (x1 & 31)) mm &= (1u << (x1 & 31)) - 1u;
-                cnt += __popc(mm);
-            }
-        }
-        return cnt;
-    };
-    auto zcr_edges = [&](int fs) {  // transitions into / out of the window's zero ends or padding
-        const int ia = fs + j0, ib = min(fs + j1, en - 1);
-        int z = 0;
-        if (ia <= ib) {
-            if (j0 > 0) z += (int)cl[ia] >= tpos;
-            if (ib < fs + L - 1) z += (int)cl[ib] >= tpos;
-        }
-        return z;
-    };
+    const float t0f = (float)t0;
     const float sE = invMf * invMf, sM = invMf;
-    for (int g = wid; g < F; g += 2 * NWAVE) {  // two frames per wave: g and g + NWAVE
-        const int g2 = g + NWAVE;
-        const bool two = g2 < F;
-        const int fs = st + g * S, fs2 = st + g2 * S;
-        const int lim = min(L, en - fs);  // samples beyond the crop are zero padding
-        const int lim2 = two ? min(L, en - fs2) : 0;
-        const int16_t *X = cl + fs, *X2 = two ? cl + fs2 : cl + fs;
-        const int lim2c = two ? lim2 : lim;
-        // E = sum w^2 x^2, M = sum w |x| with x = (k - t0) - delta (scaled by 1/M' at the end);
-        // wave-uniform trip count, 4 window positions x 2 frames per lane and iteration
-        float e0 = 0.f, m0 = 0.f, e1 = 0.f, m1 = 0.f, f0 = 0.f, n0 = 0.f, f1 = 0.f, n1 = 0.f;
-        const int nit = (max(lim, lim2) + 255) >> 8;
-        for (int it = 0; it < nit; it++) {
+    // frames in batches of R4_FB per wave: all their loads are issued before any is used.
+    // Per sample y = w_j * x (the reference's windowed frame, :329-331), E += y^2, M += |y|:
+    // the weights of a vector's 8 samples are two aligned 16-B reads from the window copy
+    // shifted by u0 mod 4; x pairs go through packed fp32 ops.
+    constexpr int R4_FB = 4, R4_VL = 3;  // frames per batch, 16-B vectors per lane and frame
+    const int vmax = cur.nvec - 1;
+    const int wrow = EXTRACT_WROW(L);
+    typedef float float2v __attribute__((ext_vector_type(2)));
+    const float2v mt = {-t0f, -t0f}, md = {-deltaf, -deltaf};
+    auto frame_vec = [&](auto padded_t, const short8 &x8, const float *wr, int jb, int lim, float2v &ea,
+                         float &ma, float &mb) {
+        constexpr bool PADDED = decltype(padded_t)::value;
+        const float4 wa = *reinterpret_cast<const float4 *>(wr + jb);
+        const float4 wb = *reinterpret_cast<const float4 *>(wr + jb + 4);
+        const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int j = it * 256 + u * 64 + lane;
-                const float2 w = wtab[min(j, L - 1)];
-                const int ka = X[min(j, lim - 1)], kb = X2[min(j, lim2c - 1)];
-                const float xa = j < lim ? (float)(ka - t0) - deltaf : 0.f;
-                const float xb = j < lim2 ? (float)(kb - t0) - deltaf : 0.f;
-                if (u & 1) {
-                    e1 = fmaf(w.y, xa * xa, e1);
-                    m1 = fmaf(w.x, fabsf(xa), m1);
-                    f1 = fmaf(w.y, xb * xb, f1);
-                    n1 = fmaf(w.x, fabsf(xb), n1);
-                } else {
-                    e0 = fmaf(w.y, xa * xa, e0);
-                    m0 = fmaf(w.x, fabsf(xa), m0);
-                    f0 = fmaf(w.y, xb * xb, f0);
-                    n0 = fmaf(w.x, fabsf(xb), n0);
-                }
+        for (int h = 0; h < 4; h++) {
+            float2v x = {(float)x8[2 * h], (float)x8[2 * h + 1]};
+            x = (x + mt) + md;  // (k - t0) exact, then - delta
+            float2v w = {wv[2 * h], wv[2 * h + 1]};
+            if (PADDED) {  // samples past the crop are zero padding
+                const int j = jb + 2 * h;  // window index of the pair's first sample
+                w.x = j < lim ? w.x : 0.f;
+                w.y = j + 1 < lim ? w.y : 0.f;
             }
+            const float2v y = w * x;
+            ea = y * y + ea;
+            ma += fabsf(y.x);
+            mb += fabsf(y.y);
         }
-        const float E1 = wave_sum(e0 + e1) * sE, M1 = wave_sum(m0 + m1) * sM;
-        const int z1 = wave_sum(zcr_words(fs)) + zcr_edges(fs);
-        if (lane == 0) {
-            c.fE[g] = E1;
-            c.fM[g] = M1;
-            c.fZ[g] = z1;
+    };
+    for (int g0 = wid; g0 < (SKIP(8) ? 0 : F); g0 += NWAVE * R4_FB) {
+        short8 xv[R4_FB][R4_VL];
+#pragma unroll
+        for (int b = 0; b < R4_FB; b++) {
+            const int g = min(g0 + b * NWAVE, F - 1);
+            const int va = (lead + st + g * S) >> 3;
+#pragma unroll
+            for (int k = 0; k < R4_VL; k++) xv[b][k] = load_vec(p, cur, min(va + lane + 64 * k, vmax));
         }
-        if (two) {
-            const float E2 = wave_sum(f0 + f1) * sE, M2 = wave_sum(n0 + n1) * sM;
-            const int z2 = wave_sum(zcr_words(fs2)) + zcr_edges(fs2);
+#pragma unroll
+        for (int b = 0; b < R4_FB; b++) {
+            const int g = g0 + b * NWAVE;
+            if (g >= F) break;  // wave-uniform
+            const int fs = st + g * S;
+            const int lim = min(L, en - fs);  // samples beyond the crop are zero padding
+            const bool padded = lim < L;
+            const int u0 = lead + fs;
+            const int va = u0 >> 3, vb = (u0 + lim - 1) >> 3;
+            const int r = u0 & 3;  // copy whose rows start at window index = -u0 (mod 4)
+            const float *wr = c.wtab + r * wrow + EXTRACT_WPAD + r;  // wr[j] = w[j], j = -7 .. L + 7
+            float2v ea = {0.f, 0.f};
+            float ma = 0.f, mb = 0.f;
+            auto frame = [&](auto pt) {
+#pragma unroll
+                for (int k = 0; k < R4_VL; k++) {
+                    const int v = va + lane + 64 * k;
+                    if (v <= vb) frame_vec(pt, xv[b][k], wr, 8 * v - u0, lim, ea, ma, mb);
+                }
+                for (int v = va + lane + 64 * R4_VL; v <= vb; v += 64)  // frames > R4_VL * 512 samples
+                    frame_vec(pt, load_vec(p, cur, v), wr, 8 * v - u0, lim, ea, ma, mb);
+            };
+            if (padded)
+                frame(BoolT<true>());
+            else
+                frame(BoolT<false>());
+            const float E1 = wave_sum(ea.x + ea.y) * sE, M1 = wave_sum(ma + mb) * sM;
+            // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in
+            // [j0, j1]) and j < lim; transitions into the window's zero ends / padding count too
+            const int ia = fs + j0, ib = min(fs + j1, en - 1);  // sample coords
+            int z = wave_sum(ia < ib ? chg_count(c.posw, ia + lead, ib + lead, lane, 64) : 0);
+            if (ia <= ib) {
+                if (j0 > 0) z += pos_bit(c.posw, ia + lead);
+                if (ib < fs + L - 1) z += pos_bit(c.posw, ib + lead);
+            }
             if (lane == 0) {
-                c.fE[g2] = E2;
-                c.fM[g2] = M2;
-                c.fZ[g2] = z2;
+                c.fE[g] = E1;
+                c.fM[g] = M1;
+                c.fZ[g] = z;
             }
         }
     }
-    PREFETCH_SLICE(3);
+    for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
     __syncthreads();
     STAMP(i, 5);
 
     // ---- R5: 15-d statistics (compute_statistics x 3, fe.py:46-62) ------------------------
     {
         // np.median: the middle order statistic (odd F) or the mean of the two middle ones;
-        // ranks of the three sequences in parallel, thread t -> (sequence t / F, element t % F)
+        // parallel ranks of the three sequences (E, M as float, ZCR as int)
         const int r0 = (F - 1) / 2, r1 = F / 2;
-        for (int t = tid; t < 3 * F; t += NT) {
-            const int sq = t / F, e = t - sq * F;
-            int r = 0;
-            double val;
-            if (sq == 2) {
-                const int x = c.fZ[e];
-#pragma unroll 8
-                for (int q = 0; q < F; q++) {
-                    const int o = c.fZ[q];
-                    r += (o < x) || (o == x && q < e);
-                }
-                val = (double)x;
-            } else {
-                const float *v = sq == 0 ? c.fE : c.fM;
-                const float x = v[e];
-#pragma unroll 8
-                for (int q = 0; q < F; q++) {
-                    const float o = v[q];
-                    r += (o < x) || (o == x && q < e);
-                }
-                val = (double)x;
+        if (SKIP(16)) {
+            if (tid < 3) sh->oslo[tid] = sh->oshi[tid] = 0.0;
+        } else if (F <= 256) {
+            ballot_select<float>([&](int j) { return c.fE[j]; }, F, r0, r1, &sh->oslo[0], &sh->oshi[0], wid, lane);
+            ballot_select<float>([&](int j) { return c.fM[j]; }, F, r0, r1, &sh->oslo[1], &sh->oshi[1], wid, lane);
+            ballot_select<int>([&](int j) { return c.fZ[j]; }, F, r0, r1, &sh->oslo[2], &sh->oshi[2], wid, lane);
+        } else {
+            rank_partial([&](int q, int j) { return q == 2 ? (float)c.fZ[j] : (q == 0 ? c.fE[j] : c.fM[j]); },
+                         3, F, c.rank, wid, lane);
+            __syncthreads();
+            for (int t = tid; t < 3 * F; t += NT) {
+                const int q = t / F, e = t - q * F;
+                const int r = c.rank[t];
+                const double val = q == 2 ? (double)c.fZ[e] : (double)(q == 0 ? c.fE[e] : c.fM[e]);
+                if (r == r0) sh->oslo[q] = val;
+                if (r == r1) sh->oshi[q] = val;
             }
-            if (r == r0) sh->oslo[sq] = val;
-            if (r == r1) sh->oshi[sq] = val;
         }
     }
     __syncthreads();
     STAMP(i, 9);
-    if (wid < 3) {
+    if (wid < 3 && !SKIP(32)) {
         double s = 0.0, mx = -INFINITY, mn = INFINITY;
         for (int q = lane; q < F; q += 64) {
             const double x = wid == 0 ? (double)c.fE[q] : wid == 1 ? (double)c.fM[q] : (double)c.fZ[q];
@@ -1065,105 +1091,133 @@ __device__ __forceinline__ void write_bad_clip(const ExtractParams &p, int i, in
     }
 }
 
-__global__ __launch_bounds__(NT) void extract_kernel(ExtractParams p)
+__device__ __forceinline__ void issue_clip(short8 (&regs)[NRV], const ExtractParams &p, const ClipRef &c)
 {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+#pragma unroll
+    for (int r = 0; r < RREG; r++) issue_word(&regs[4 * r], p, c, r * NT + (int)threadIdx.x);
+}
+
+__device__ __forceinline__ Ctx make_ctx(const ExtractParams &p, unsigned char *lds)
+{
     const ExtractCarve cv = extract_carve(p.ncap, p.L, p.S, EXTRACT_DEFER_CAP);
     Ctx c;
     c.sh = reinterpret_cast<Shared *>(lds + cv.sh);
-    c.buf = reinterpret_cast<int16_t *>(lds + cv.clip);
-    c.chg = reinterpret_cast<uint32_t *>(lds + cv.chg);
-    c.pos = c.chg;  // positive bits are turned into change bits in place
-    c.sgQ = reinterpret_cast<unsigned long long *>(lds + cv.seg);
-    c.sgS = reinterpret_cast<int *>(c.sgQ + cv.nseg);
-    c.sgZ = c.sgS + cv.nseg;
-    c.wtab = reinterpret_cast<float2 *>(lds + cv.wtab);
+    c.wtab = reinterpret_cast<const float *>(lds + cv.wtab);
+    c.posw = reinterpret_cast<uint32_t *>(lds + cv.posw);
+    c.wS2 = reinterpret_cast<unsigned long long *>(lds + cv.wS2);
+    c.wS1 = reinterpret_cast<int *>(lds + cv.wS1);
     c.vE = reinterpret_cast<double *>(lds + cv.vE);
     c.vZ = reinterpret_cast<int32_t *>(lds + cv.vZ);
     c.fE = reinterpret_cast<float *>(lds + cv.fE);
     c.fM = reinterpret_cast<float *>(lds + cv.fM);
     c.fZ = reinterpret_cast<int32_t *>(lds + cv.fZ);
+    c.rank = reinterpret_cast<int *>(lds + cv.rank);
     c.defer = reinterpret_cast<int *>(lds + cv.defer);
-    c.total = p.offsets[p.B];
+    c.total = 0;
+    c.stamp_clip = 0;
+    return c;
+}
+
+// the rare near-tie redo, compiled out of line so its exact-order machinery does not weigh on
+// the register allocation of the streaming path
+__device__ __attribute__((noinline)) void clip_exact(const ExtractParams p, int i)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    Ctx c = make_ctx(p, lds);
+    c.stamp_clip = i;
+    const ClipRef cr = clip_ref(p, i);
+    short8 regs[NRV];
+    issue_clip(regs, p, cr);
+    clip_body<true>(p, c, i, cr, regs);
+}
+
+// 128 VGPRs: two 512-thread workgroups per CU
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void extract_kernel(ExtractParams p)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const ExtractCarve cv = extract_carve(p.ncap, p.L, p.S, EXTRACT_DEFER_CAP);
+    float *wt = reinterpret_cast<float *>(lds + cv.wtab);
+    Ctx c = make_ctx(p, lds);
     Shared *sh = c.sh;
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int L = p.L, G = gridDim.x;
 
-    // window (create_window, :278-296) -> LDS once; its support [j0, j1] via ballots
+    // window (create_window, :278-296) -> LDS once as four shifted zero-padded fp32 copies; its
+    // support [j0, j1] by ballots
     if (tid == 0) {
         sh->j0 = L;
         sh->j1 = -1;
         sh->ndefer = 0;
     }
     __syncthreads();
+    const int wrow = EXTRACT_WROW(L);
+    for (int m = tid; m < 4 * wrow; m += NT) {
+        const int r = m / wrow, j = m - r * wrow - EXTRACT_WPAD - r;
+        wt[m] = (j >= 0 && j < L) ? (float)p.window[j] : 0.f;
+    }
     for (int q0 = wid * 64; q0 < L; q0 += NT) {
         const int j = q0 + lane;
-        const double w = j < L ? p.window[j] : 0.0;
-        if (j < L) {
-            c.wtab[j] = make_float2((float)w, (float)(w * w));
-        }
-        const unsigned long long m = __ballot(j < L && w > 0.0);
+        const bool in = j < L;
+        const double w = in ? p.window[j] : 0.0;
+        const unsigned long long m = __ballot(in && w > 0.0);
         if (lane == 0 && m) {
             atomicMin(&sh->j0, q0 + __ffsll((long long)m) - 1);
             atomicMax(&sh->j1, q0 + 63 - __clzll((long long)m));
         }
     }
+    __syncthreads();
 
-    short8 regs[NPF];
-    int i = blockIdx.x;
-    ClipRef cur;
-    if (i < p.B) {
-        cur = clip_ref(p, i, c.total);
-        issue_loads(regs, p.pcm, cur, tid);
-    }
-    for (; i < p.B; i += G) {
-        const bool has_next = i + G < p.B;
-        const ClipRef nxt = has_next ? clip_ref(p, i + G, c.total) : ClipRef{0, 0, 0, 0, 0, false};
+    short8 regs[NRV];
+    for (int i = blockIdx.x; i < p.B; i += G) {
+        const ClipRef cur = clip_ref(p, i);
         if (!cur.ok) {
             write_bad_clip(p, i, tid);
-            if (has_next) issue_loads(regs, p.pcm, nxt, tid);
-        } else {
-            const bool done = clip_body<false>(p, c, i, cur, regs, has_next, nxt);
-            if (!done && tid == 0) {
-                if (sh->ndefer < EXTRACT_DEFER_CAP) {
-                    c.defer[sh->ndefer++] = i;
-                } else {  // list full (> EXTRACT_DEFER_CAP near ties in one workgroup)
-                    p.status[i] = DSP_CLIP_UNCERTIFIED;
-                }
-            }
-            __syncthreads();  // LDS is rewritten by the next clip
+            continue;
         }
-        cur = nxt;
+        issue_clip(regs, p, cur);
+        c.stamp_clip = i;
+        const bool done = clip_body<false>(p, c, i, cur, regs);
+        if (!done && tid == 0) {
+            if (sh->ndefer < EXTRACT_DEFER_CAP) {
+                c.defer[sh->ndefer++] = i;
+            } else {  // list full (> EXTRACT_DEFER_CAP near ties in one workgroup)
+                p.status[i] = DSP_CLIP_UNCERTIFIED;
+            }
+        }
+        __syncthreads();  // LDS summaries are rewritten by the next clip
     }
-    // near ties (rare): endpoint energies in numpy's exact float64 order, no prefetch live
+    // near ties (rare): endpoint energies in numpy's exact float64 order
     __syncthreads();
     const int nd = sh->ndefer;
     for (int d = 0; d < nd; d++) {
         const int j = c.defer[d];
-        const ClipRef cr = clip_ref(p, j, c.total);
-        clip_body<true>(p, c, j, cr, regs, false, cr);
+        clip_exact(p, j);
         __syncthreads();
     }
 }
 
 }  // namespace dsp
 
+static void *g_stamp_buffer = nullptr;
+static int g_skip = 0;
 #ifdef DSP_STAMPS
 extern "C" int dsp_debug_set_stamp_buffer(void *buf)
 {
-    return (int)hipMemcpyToSymbol(HIP_SYMBOL(dsp::g_stamps), &buf, sizeof(buf));
+    g_stamp_buffer = buf;
+    return 0;
 }
-extern "C" int dsp_debug_set_dump_buffer(void *buf)
+extern "C" int dsp_debug_set_skip(int mask)
 {
-    return (int)hipMemcpyToSymbol(HIP_SYMBOL(dsp::g_dump), &buf, sizeof(buf));
+    g_skip = mask;
+    return 0;
 }
 #endif
 
 extern "C" size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int frame_shift)
 {
     if (max_len < 1 || frame_length < 1 || frame_shift < 1) return 0;
-    if (max_len + 16 > (int64_t)8 * EXTRACT_MAX_ROUNDS * EXTRACT_THREADS) return 0;
+    if (max_len > (1 << 24) || frame_length > (1 << 20)) return 0;
     const ExtractCarve c = extract_carve((int)max_len, frame_length, frame_shift, EXTRACT_DEFER_CAP);
     return c.total <= EXTRACT_LDS_LIMIT ? (size_t)c.total : 0;
 }
@@ -1217,10 +1271,15 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     p.ld_vad = ld_vad;
     p.seq = seq;
     p.ld_seq = ld_seq;
-    // persistent grid: one workgroup per CU (the LDS footprint admits one), each walks clips
-    // blockIdx, blockIdx + grid, ...
-    const int grid = B < g_num_cus ? B : g_num_cus;
+    p.stamps = (unsigned long long *)g_stamp_buffer;
+    p.skip = g_skip;
+    // persistent grid: two workgroups per CU when their LDS fits (one otherwise), each walking
+    // clips blockIdx, blockIdx + grid, ...
+    const int per_cu = lds <= EXTRACT_LDS_SHARED ? 2 : 1;
+    const int slots = per_cu * g_num_cus;
+    const int grid = B < slots ? B : slots;
     hipLaunchKernelGGL(dsp::extract_kernel, dim3(grid), dim3(dsp::NT), lds, (hipStream_t)stream, p);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? DSP_OK : DSP_ERR_HIP + (int)e;
 }
+

@@ -1,23 +1,30 @@
-// extract_layout.h -- LDS carve-up of the fused extraction kernel, shared by host and device.
+// LDS carve-up of the extraction kernel (host and device agree on it).
+//
+// The clip itself is NOT in LDS: it is held in registers (EXTRACT_RREG 32-sample words per
+// thread) for the two passes that need every sample, and re-read from L2 by the phases that need
+// a few (crop frames, partial words at VAD frame edges).  LDS holds per-word summaries (positive-
+// sample bits, exact moments) and the small per-frame arrays, ~36 KB for a 1 s clip, so two
+// workgroups share a CU.
 #ifndef DSP_EXTRACT_LAYOUT_H
 #define DSP_EXTRACT_LAYOUT_H
 
-#include <hip/hip_runtime.h>
-
 #define EXTRACT_THREADS 512
-#define EXTRACT_LDS_LIMIT (160 * 1024)
-#define EXTRACT_MAX_ROUNDS 20   // 16-B loads per thread: clips up to 8*20*512-16 samples
-#define EXTRACT_PREFETCH 12     // of which prefetched into registers (clips <= 49136 samples)
-#define EXTRACT_DEFER_CAP 512   // near-tie clips one workgroup can redo exactly
-#define EXTRACT_SHARED_BYTES 512  // sizeof(dsp::Shared) rounded up (static_assert'ed)
+#define EXTRACT_RREG 3                   // 32-sample words per thread held in registers
+#define EXTRACT_LDS_LIMIT (160 * 1024)   // one CU
+#define EXTRACT_LDS_SHARED (80 * 1024)   // per workgroup when two share a CU
+#define EXTRACT_DEFER_CAP 256            // near-tie clips one workgroup can redo exactly
+#define EXTRACT_SHARED_BYTES 512         // sizeof(dsp::Shared) rounded up (static_assert'ed)
+#define EXTRACT_WPAD 8                   // zero window entries on each side of the window table
+// floats per shifted window copy: copy r holds w[m - WPAD - r] at m (zero outside [0, L)), so
+// that 4 consecutive weights starting at any window index are one aligned 16-B LDS read
+#define EXTRACT_WROW(L) ((((L) + 2 * EXTRACT_WPAD + 4) + 3) & ~3)
 
 struct ExtractCarve {
-    int sh, clip, wtab, chg, seg, vE, vZ, fE, fM, fZ, defer, total;
-    int nvcap, fcap, nvecmax, nseg;
+    int sh, wtab, posw, wS2, wS1, vE, vZ, fE, fM, fZ, rank, defer, total;
+    int nvcap, fcap, nwmax;
 };
 
-// ncap: longest clip (samples); L, S: frame length / shift (samples);
-// per_wg: clips one persistent workgroup walks (sizes the deferred-clip list)
+// ncap = longest clip of the launch (samples)
 __host__ __device__ inline ExtractCarve extract_carve(int ncap, int L, int S, int per_wg)
 {
     ExtractCarve c;
@@ -29,18 +36,18 @@ __host__ __device__ inline ExtractCarve extract_carve(int ncap, int L, int S, in
     } while (0)
     c.nvcap = ncap >= L ? (ncap - L) / S + 1 : 0;
     c.fcap = ncap <= L ? 1 : (ncap - L + S - 1) / S + 1;
-    c.nvecmax = (ncap + 7 + 7) / 8 + 1;     // 16-B vectors incl. alignment lead
-    c.nseg = 2 * (c.nvcap + L / S + 1);     // hop segments [qS, qS+r), [qS+r, (q+1)S)
+    c.nwmax = (ncap + 7 + 31) / 32 + 1;  // 32-sample words incl. the alignment lead
     DSP_TAKE(sh, EXTRACT_SHARED_BYTES);
-    DSP_TAKE(clip, 16 * c.nvecmax + 32);    // int16, buffer coordinates (lead <= 7)
-    DSP_TAKE(wtab, 8 * L);                  // (window, window^2) pairs
-    DSP_TAKE(chg, c.nvecmax + 16);          // positive bits, then sign-change bits (in place)
-    DSP_TAKE(seg, 16 * c.nseg);             // per segment: sum k^2 (u64), sum k, sign changes
+    DSP_TAKE(wtab, 16 * EXTRACT_WROW(L));          // 4 zero-padded copies of w, shifted by 0..3
+    DSP_TAKE(posw, 4 * (c.nwmax + 2));           // positive-sample bits (+2 zero sentinels)
+    DSP_TAKE(wS2, 8 * c.nwmax);                  // per word: sum k^2 (exact, u64)
+    DSP_TAKE(wS1, 4 * c.nwmax);                  // per word: sum k
     DSP_TAKE(vE, 8 * c.nvcap);
     DSP_TAKE(vZ, 4 * c.nvcap);
     DSP_TAKE(fE, 4 * c.fcap);
     DSP_TAKE(fM, 4 * c.fcap);
     DSP_TAKE(fZ, 4 * c.fcap);
+    DSP_TAKE(rank, 4 * (c.nvcap > 3 * c.fcap ? c.nvcap : 3 * c.fcap));
     DSP_TAKE(defer, 4 * per_wg);
 #undef DSP_TAKE
     c.total = o;

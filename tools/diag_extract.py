@@ -27,9 +27,12 @@ if STAMPS:
     assert L_.dsp_debug_set_stamp_buffer(ctypes.c_void_p(stamp_buf.data_ptr())) == 0
 x = torch.as_tensor(make_batch(C, base_seed=0)).cuda()
 res = {}
+ONLY = os.environ.get("DIAG_VARIANTS")
 for name, kw in [("vad_hamming", dict(window_type="hamming", do_endpoint_detection=True)),
                  ("novad_hamming", dict(window_type="hamming", do_endpoint_detection=False)),
                  ("vad_rect", dict(window_type="rectangular", do_endpoint_detection=True))]:
+    if ONLY and name not in ONLY.split(","):
+        continue
     fx = FeatureExtractor(1102, 441, **kw)
     out = fx(x)
     st = out["status"].cpu().numpy()
@@ -38,17 +41,15 @@ for name, kw in [("vad_hamming", dict(window_type="hamming", do_endpoint_detecti
         stamp_buf.zero_(); fx(x); torch.cuda.synchronize()
         st_ = stamp_buf.cpu().numpy().astype(np.float64)
         ph = {}
-        seq = [0, 1, 2, 7, 8, 3, 4, 5, 9, 6]
-        names = ["R1 load+stats", "R2a pos+chg", "R2b segments", "R3a vad frames", "R3 p90 rank",
-                 "R3b scan", "R4 features", "R5 median ranks", "R5 stats+out"]
-        for k in range(len(seq) - 1):
-            a_, b_ = seq[k], seq[k + 1]
+        # stamp ids in program order and the phase each one ends
+        seq = [0, 1, 2, 7, 8, 3, 10, 11, 4, 5, 9, 6]
+        names = {1: "R1 load+stats", 2: "R2a pos+chg", 7: "R2b segments", 8: "R3a vad frames",
+                 3: "R3 p90 rank", 10: "R3b noise+thresholds", 11: "R3b ballots", 4: "R3b barrier+out",
+                 5: "R4 features", 9: "R5 median ranks", 6: "R5 stats+out"}
+        present = [k for k in seq if (st_[:, k] > 0).any()]
+        for a_, b_ in zip(present, present[1:]):
             ok = (st_[:, a_] > 0) & (st_[:, b_] > 0)
-            if ok.any(): ph[names[k]] = float(np.median(st_[ok, b_] - st_[ok, a_]))
-        # VAD off: stamps 7/8/3/4 missing -> bridge 2 -> 5 when absent
-        if not ((st_[:, 7] > 0).any()):
-            ok = (st_[:, 2] > 0) & (st_[:, 5] > 0)
-            ph["R4 features (from R2a)"] = float(np.median(st_[ok, 5] - st_[ok, 2]))
+            ph[names[b_]] = float(np.median(st_[ok, b_] - st_[ok, a_]))
         ok = (st_[:, 0] > 0) & (st_[:, 6] > 0)
         ph["total"] = float(np.median(st_[ok, 6] - st_[ok, 0]))
         # clip-to-clip period on one workgroup (includes the wait for the prefetched loads)
