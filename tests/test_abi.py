@@ -44,8 +44,9 @@ def test_abi_version(lib):
 def test_lds_sizing(lib):
     assert lib.dsp_extract_lds_bytes(44100, 1102, 441) > 0
     assert lib.dsp_extract_lds_bytes(44100, 1024, 512) > 0
-    assert lib.dsp_extract_lds_bytes(66150, 1102, 441) <= 160 * 1024
-    assert lib.dsp_extract_lds_bytes(200000, 1102, 441) == 0  # beyond one CU's LDS
+    assert lib.dsp_extract_lds_bytes(44100, 1102, 441) <= 80 * 1024  # two workgroups per CU
+    assert 0 < lib.dsp_extract_lds_bytes(200000, 1102, 441) <= 160 * 1024  # 4.5 s: summaries only
+    assert lib.dsp_extract_lds_bytes(400000, 1102, 441) == 0  # beyond one CU's LDS
     assert lib.dsp_extract_lds_bytes(0, 1102, 441) == 0
     assert lib.dsp_extract_lds_bytes(44100, 0, 441) == 0
 
