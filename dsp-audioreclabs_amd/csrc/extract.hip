@@ -77,6 +77,9 @@ typedef short short8 __attribute__((ext_vector_type(8)));
 template <bool B> struct BoolT {
     static constexpr bool value = B;
 };
+template <int K> struct IntT {
+    static constexpr int value = K;
+};
 typedef short short2v __attribute__((ext_vector_type(2)));
 
 // ---- wave reductions on DPP (VALU lane permutes, no LDS crossbar) + 4 readlanes -------------
@@ -380,6 +383,7 @@ __device__ __forceinline__ int chg_count(const uint32_t *posw, int x0, int x1, i
     int c = 0;
     if (x1 > x0) {
         const int w0 = x0 >> 5, w1 = (x1 - 1) >> 5;
+#pragma unroll 3
         for (int w = w0 + l0; w <= w1; w += nl) {
             uint32_t m = chg_word(posw, w);
             if (w == w0) m &= ~0u << (x0 & 31);
@@ -391,14 +395,15 @@ __device__ __forceinline__ int chg_count(const uint32_t *posw, int x0, int x1, i
 }
 __device__ __forceinline__ int pos_bit(const uint32_t *posw, int u) { return (posw[u >> 5] >> (u & 31)) & 1; }
 
-// ---- 256-frame bit sets (wave-uniform: four ballots) ------------------------------------------
-struct Bits256 {
-    unsigned long long w[4];
+// ---- frame bit sets of KC ballots (wave-uniform), KC * 64 frames --------------------------
+template <int KC> struct BitsK {
+    unsigned long long w[KC];
 };
-__device__ __forceinline__ int bits_first_ge(const Bits256 &m, int from)  // lowest set >= from, or -1
+template <int KC>
+__device__ __forceinline__ int bits_first_ge(const BitsK<KC> &m, int from)  // lowest set >= from, or -1
 {
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < KC; k++) {
         const int sh = from - 64 * k;
         unsigned long long x = m.w[k];
         if (sh >= 64) x = 0;
@@ -407,10 +412,11 @@ __device__ __forceinline__ int bits_first_ge(const Bits256 &m, int from)  // low
     }
     return -1;
 }
-__device__ __forceinline__ int bits_last_lt(const Bits256 &m, int below)  // highest set < below, or -1
+template <int KC>
+__device__ __forceinline__ int bits_last_lt(const BitsK<KC> &m, int below)  // highest set < below, or -1
 {
 #pragma unroll
-    for (int k = 3; k >= 0; k--) {
+    for (int k = KC - 1; k >= 0; k--) {
         const int sh = below - 64 * k;
         unsigned long long x = m.w[k];
         if (sh <= 0) x = 0;
@@ -419,7 +425,8 @@ __device__ __forceinline__ int bits_last_lt(const Bits256 &m, int below)  // hig
     }
     return -1;
 }
-__device__ __forceinline__ bool bits_any_in(const Bits256 &m, int lo, int hi)  // any set in [lo, hi)
+template <int KC>
+__device__ __forceinline__ bool bits_any_in(const BitsK<KC> &m, int lo, int hi)  // any set in [lo, hi)
 {
     const int f = bits_first_ge(m, lo);
     return f >= 0 && f < hi;
@@ -470,10 +477,11 @@ __device__ __forceinline__ int vad_scan(const ExtractParams &p, const Ctx &c, in
         return d <= 1e-11 * fmax(fabs(e), fabs(t)) && !(e == 0.0 && t == 0.0);
     };
     int flag = 0, n3 = -1, n1 = 0, n6 = nv - 1;
-    if (nv <= 256) {
-        Bits256 hiE, loE, loZ, nr1, nr2;
+    auto short_scan = [&](auto kc_t) {
+        constexpr int KC = decltype(kc_t)::value;
+        BitsK<KC> hiE, loE, loZ, nr1, nr2;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < KC; k++) {
             const int q = 64 * k + lane;
             const bool in = q < nv;
             const double e = in ? vE[q] : 0.0;
@@ -502,6 +510,11 @@ __device__ __forceinline__ int vad_scan(const ExtractParams &p, const Ctx &c, in
             const int b6 = bits_first_ge(loZ, n5 + 1);  // :258-265
             n6 = b6 >= 0 ? b6 - 1 : nv - 1;
         }
+    };
+    if (nv <= 128) {
+        short_scan(IntT<2>());
+    } else if (nv <= 256) {
+        short_scan(IntT<4>());
     } else {  // long sequences: chunked ballots straight from LDS
         int n4 = -1;
         for (int q0 = 0; q0 < nv; q0 += 64) {
@@ -609,6 +622,84 @@ __device__ __forceinline__ long long dpp_quad_sum_i64(long long v)
     return (long long)dpp_quad_sum64((unsigned long long)v);
 }
 
+// ---- order statistics by an in-wave bitonic sort -------------------------------------------
+// Keys are unsigned integers whose order is the value order (equal keys <=> equal values, so
+// ties need no index), two per lane at most (element lane + 64h in a[h]); pad with the max key.
+__device__ __forceinline__ unsigned long long dkey(double v)
+{
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+__device__ __forceinline__ double dkey_value(unsigned long long k)
+{
+    return __builtin_bit_cast(double, (k >> 63) ? (k & ~(1ull << 63)) : ~k);
+}
+__device__ __forceinline__ unsigned fkey(float v)
+{
+    const unsigned b = __builtin_bit_cast(unsigned, v);
+    return (b >> 31) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_value(unsigned k)
+{
+    return __builtin_bit_cast(float, (k >> 31) ? (k & 0x7FFFFFFFu) : ~k);
+}
+// value of lane ^ m without the LDS crossbar: DPP for 1, 2, 8, swizzle for 4, the gfx950
+// permlane swaps for 16, 32 (checked against __shfl_xor by tools/ubench/perm_check.hip)
+__device__ __forceinline__ unsigned shfl_xor_k(unsigned v, int m, int lane)
+{
+    const int x = (int)v;
+    switch (m) {
+    case 1: return (unsigned)__builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);
+    case 2: return (unsigned)__builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);
+    case 4: return (unsigned)__builtin_amdgcn_ds_swizzle(x, 0x101F);
+    case 8: return (unsigned)__builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);
+    case 16: {
+        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return (unsigned)((lane & 16) ? r[0] : r[1]);
+    }
+    default: {
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (unsigned)((lane & 32) ? r[0] : r[1]);
+    }
+    }
+}
+__device__ __forceinline__ unsigned long long shfl_xor_k(unsigned long long v, int m, int lane)
+{
+    const unsigned lo = shfl_xor_k((unsigned)v, m, lane), hi = shfl_xor_k((unsigned)(v >> 32), m, lane);
+    return ((unsigned long long)hi << 32) | lo;
+}
+template <int NH, typename K>
+__device__ __forceinline__ void wave_bitonic(K (&a)[NH], int lane)
+{
+    constexpr int N = 64 * NH;
+#pragma unroll
+    for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (NH == 2 && stride == 64) {  // partner in the same lane; size == 128: ascending
+                const bool sw = a[NH - 1] < a[0];
+                const K lo = sw ? a[NH - 1] : a[0], hi = sw ? a[0] : a[NH - 1];
+                a[0] = lo;
+                a[NH - 1] = hi;
+            } else {
+#pragma unroll
+                for (int h = 0; h < NH; h++) {
+                    const int i = lane + 64 * h;
+                    const K q = shfl_xor_k(a[h], stride, lane);
+                    const bool takemin = ((i & stride) == 0) == ((i & size) == 0);
+                    const bool qless = q < a[h];
+                    a[h] = (takemin == qless) ? q : a[h];
+                }
+            }
+        }
+    }
+}
+template <int NH, typename K>
+__device__ __forceinline__ K sorted_at(const K (&a)[NH], int r)  // wave-uniform r
+{
+    return lane_read((NH == 2 && r >= 64) ? a[NH - 1] : a[0], r & 63);
+}
+
 // Order statistics r0 / r1 (ranks with ties broken by index) of v[0..n), n <= 256: every wave
 // holds the whole sequence in registers (lane + 64k), wave w ranks elements w, w + NWAVE, ...
 // with one ballot per chunk.  Lane 0 of the wave that finds them stores them.
@@ -624,7 +715,8 @@ __device__ __forceinline__ void ballot_select(Get get, int n, int r0, int r1, do
     }
     const int kc = (n + 63) >> 6;
     for (int i = wid; i < n; i += NWAVE) {
-        const T e = get(i);
+        const int ki = i >> 6;
+        const T e = lane_read(ki == 0 ? x[0] : ki == 1 ? x[1] : ki == 2 ? x[2] : x[3], i & 63);
         int r = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -871,6 +963,18 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
             }
             if (SKIP(2)) {
                 if (tid == 0) sh->pa = sh->pb = c.vE[r0];
+            } else if (nv <= 128) {  // wave 0: bitonic sort of the energies, then the scan below
+                if (wid == 0) {
+                    unsigned long long a[2];
+                    a[0] = lane < nv ? dkey(c.vE[lane]) : ~0ull;
+                    a[1] = lane + 64 < nv ? dkey(c.vE[lane + 64]) : ~0ull;
+                    wave_bitonic<2>(a, lane);
+                    const double pa = dkey_value(sorted_at<2>(a, r0)), pb = dkey_value(sorted_at<2>(a, r1));
+                    if (lane == 0) {
+                        sh->pa = pa;
+                        sh->pb = pb;
+                    }
+                }
             } else if (nv <= 256) {
                 ballot_select<double>([&](int j) { return c.vE[j]; }, nv, r0, r1, &sh->pa, &sh->pb, wid, lane);
             } else {  // long clips: partial ranks over all waves
@@ -883,7 +987,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                 }
             }
         }
-        __syncthreads();
+        if (nv > 128 || SKIP(2)) __syncthreads();  // (wave 0 alone wrote pa / pb otherwise)
         STAMP(i, 3);
         if (SKIP(4)) {
             if (tid == 0) {
@@ -920,11 +1024,9 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     const int j0 = sh->j0, j1 = sh->j1;
     const float t0f = (float)t0;
     const float sE = invMf * invMf, sM = invMf;
-    // frames in batches of R4_FB per wave: all their loads are issued before any is used.
     // Per sample y = w_j * x (the reference's windowed frame, :329-331), E += y^2, M += |y|:
     // the weights of a vector's 8 samples are two aligned 16-B reads from the window copy
     // shifted by u0 mod 4; x pairs go through packed fp32 ops.
-    constexpr int R4_FB = 4, R4_VL = 3;  // frames per batch, 16-B vectors per lane and frame
     const int vmax = cur.nvec - 1;
     const int wrow = EXTRACT_WROW(L);
     typedef float float2v __attribute__((ext_vector_type(2)));
@@ -951,117 +1053,146 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
             mb += fabsf(y.y);
         }
     };
-    for (int g0 = wid; g0 < (SKIP(8) ? 0 : F); g0 += NWAVE * R4_FB) {
-        short8 xv[R4_FB][R4_VL];
+    // one 16-lane row per frame (4 frames per wave): lane rl of the row takes the frame's vectors
+    // va + rl + 16k; every vector load of the frame is issued before any is used, and the row
+    // sums need four DPP steps instead of a wave reduction
+    constexpr int R4_KV = 9;  // vectors per lane in one batch (frames up to 16*9*8-7 samples)
+    const int rl = lane & 15, row = lane >> 4;
+    for (int gi = wid; 4 * gi < (SKIP(8) ? 0 : F); gi += NWAVE) {
+        const int g = 4 * gi + row;
+        const bool act = g < F;
+        const int gc = act ? g : F - 1;
+        const int fs = st + gc * S;
+        const int lim = min(L, en - fs);  // samples beyond the crop are zero padding
+        const bool padded = lim < L;
+        const int u0 = lead + fs;
+        const int va = u0 >> 3, vb = (u0 + lim - 1) >> 3;
+        const int r = u0 & 3;  // copy whose rows start at window index = -u0 (mod 4)
+        const float *wr = c.wtab + r * wrow + EXTRACT_WPAD + r;  // wr[j] = w[j], j = -7 .. L + 7
+        float2v ea = {0.f, 0.f};
+        float ma = 0.f, mb = 0.f;
+        for (int v0 = va; v0 <= vb; v0 += 16 * R4_KV) {
+            short8 xv[R4_KV];
 #pragma unroll
-        for (int b = 0; b < R4_FB; b++) {
-            const int g = min(g0 + b * NWAVE, F - 1);
-            const int va = (lead + st + g * S) >> 3;
+            for (int k = 0; k < R4_KV; k++) xv[k] = load_vec(p, cur, min(v0 + rl + 16 * k, vmax));
+            auto run = [&](auto pt) {
 #pragma unroll
-            for (int k = 0; k < R4_VL; k++) xv[b][k] = load_vec(p, cur, min(va + lane + 64 * k, vmax));
-        }
-#pragma unroll
-        for (int b = 0; b < R4_FB; b++) {
-            const int g = g0 + b * NWAVE;
-            if (g >= F) break;  // wave-uniform
-            const int fs = st + g * S;
-            const int lim = min(L, en - fs);  // samples beyond the crop are zero padding
-            const bool padded = lim < L;
-            const int u0 = lead + fs;
-            const int va = u0 >> 3, vb = (u0 + lim - 1) >> 3;
-            const int r = u0 & 3;  // copy whose rows start at window index = -u0 (mod 4)
-            const float *wr = c.wtab + r * wrow + EXTRACT_WPAD + r;  // wr[j] = w[j], j = -7 .. L + 7
-            float2v ea = {0.f, 0.f};
-            float ma = 0.f, mb = 0.f;
-            auto frame = [&](auto pt) {
-#pragma unroll
-                for (int k = 0; k < R4_VL; k++) {
-                    const int v = va + lane + 64 * k;
-                    if (v <= vb) frame_vec(pt, xv[b][k], wr, 8 * v - u0, lim, ea, ma, mb);
+                for (int k = 0; k < R4_KV; k++) {
+                    const int v = v0 + rl + 16 * k;
+                    if (v <= vb) frame_vec(pt, xv[k], wr, 8 * v - u0, lim, ea, ma, mb);
                 }
-                for (int v = va + lane + 64 * R4_VL; v <= vb; v += 64)  // frames > R4_VL * 512 samples
-                    frame_vec(pt, load_vec(p, cur, v), wr, 8 * v - u0, lim, ea, ma, mb);
             };
             if (padded)
-                frame(BoolT<true>());
+                run(BoolT<true>());
             else
-                frame(BoolT<false>());
-            const float E1 = wave_sum(ea.x + ea.y) * sE, M1 = wave_sum(ma + mb) * sM;
-            // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in
-            // [j0, j1]) and j < lim; transitions into the window's zero ends / padding count too
-            const int ia = fs + j0, ib = min(fs + j1, en - 1);  // sample coords
-            int z = wave_sum(ia < ib ? chg_count(c.posw, ia + lead, ib + lead, lane, 64) : 0);
-            if (ia <= ib) {
-                if (j0 > 0) z += pos_bit(c.posw, ia + lead);
-                if (ib < fs + L - 1) z += pos_bit(c.posw, ib + lead);
-            }
-            if (lane == 0) {
-                c.fE[g] = E1;
-                c.fM[g] = M1;
-                c.fZ[g] = z;
-            }
+                run(BoolT<false>());
+        }
+        const float E1 = dpp_row_reduce(ea.x + ea.y, OpAdd()) * sE;
+        const float M1 = dpp_row_reduce(ma + mb, OpAdd()) * sM;
+        // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in
+        // [j0, j1]) and j < lim; transitions into the window's zero ends / padding count too
+        const int ia = fs + j0, ib = min(fs + j1, en - 1);  // sample coords
+        int z = dpp_row_reduce(ia < ib ? chg_count(c.posw, ia + lead, ib + lead, rl, 16) : 0, OpAdd());
+        if (ia <= ib) {
+            if (j0 > 0) z += pos_bit(c.posw, ia + lead);
+            if (ib < fs + L - 1) z += pos_bit(c.posw, ib + lead);
+        }
+        if (act && rl == 0) {
+            c.fE[g] = E1;
+            c.fM[g] = M1;
+            c.fZ[g] = z;
         }
     }
-    for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
+    if (F > 128)
+        for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
     __syncthreads();
     STAMP(i, 5);
 
     // ---- R5: 15-d statistics (compute_statistics x 3, fe.py:46-62) ------------------------
-    {
-        // np.median: the middle order statistic (odd F) or the mean of the two middle ones;
-        // parallel ranks of the three sequences (E, M as float, ZCR as int)
-        const int r0 = (F - 1) / 2, r1 = F / 2;
-        if (SKIP(16)) {
-            if (tid < 3) sh->oslo[tid] = sh->oshi[tid] = 0.0;
-        } else if (F <= 256) {
-            ballot_select<float>([&](int j) { return c.fE[j]; }, F, r0, r1, &sh->oslo[0], &sh->oshi[0], wid, lane);
-            ballot_select<float>([&](int j) { return c.fM[j]; }, F, r0, r1, &sh->oslo[1], &sh->oshi[1], wid, lane);
-            ballot_select<int>([&](int j) { return c.fZ[j]; }, F, r0, r1, &sh->oslo[2], &sh->oshi[2], wid, lane);
-        } else {
-            rank_partial([&](int q, int j) { return q == 2 ? (float)c.fZ[j] : (q == 0 ? c.fE[j] : c.fM[j]); },
-                         3, F, c.rank, wid, lane);
-            __syncthreads();
-            for (int t = tid; t < 3 * F; t += NT) {
-                const int q = t / F, e = t - q * F;
-                const int r = c.rank[t];
-                const double val = q == 2 ? (double)c.fZ[e] : (double)(q == 0 ? c.fE[e] : c.fM[e]);
-                if (r == r0) sh->oslo[q] = val;
-                if (r == r1) sh->oshi[q] = val;
+    // np.median: the middle order statistic (odd F) or the mean of the two middle ones
+    const int r0 = (F - 1) / 2, r1 = F / 2;
+    if (F <= 128) {
+        // wave q alone handles sequence q (E, M, ZCR): lanes hold v[lane], v[lane + 64]; the
+        // order statistics by ballot ranks over readlane'd candidates, then mean / std (fp64 sums)
+        // and max / min -- no barrier
+        if (wid < 3 && !SKIP(48)) {
+            const int q = wid;
+            auto get = [&](int j) -> float { return q == 0 ? c.fE[j] : q == 1 ? c.fM[j] : (float)c.fZ[j]; };
+            const bool in0 = lane < F, in1 = lane + 64 < F;
+            const float x0 = in0 ? get(lane) : 0.f, x1 = in1 ? get(lane + 64) : 0.f;
+            unsigned a[2] = {in0 ? fkey(x0) : ~0u, in1 ? fkey(x1) : ~0u};
+            float v0, v1;
+            if (F <= 64) {
+                unsigned b[1] = {a[0]};
+                wave_bitonic<1>(b, lane);
+                v0 = fkey_value(sorted_at<1>(b, r0));
+                v1 = fkey_value(sorted_at<1>(b, r1));
+            } else {
+                wave_bitonic<2>(a, lane);
+                v0 = fkey_value(sorted_at<2>(a, r0));
+                v1 = fkey_value(sorted_at<2>(a, r1));
+            }
+            const double s = wave_sum((in0 ? (double)x0 : 0.0) + (in1 ? (double)x1 : 0.0));
+            const float mx = wave_reduce(fmaxf(in0 ? x0 : -INFINITY, in1 ? x1 : -INFINITY), OpMax());
+            const float mn = wave_reduce(fminf(in0 ? x0 : INFINITY, in1 ? x1 : INFINITY), OpMin());
+            const double mean = s / (double)F;
+            const double d0 = in0 ? (double)x0 - mean : 0.0, d1 = in1 ? (double)x1 - mean : 0.0;
+            const double qq = wave_sum(fma(d0, d0, d1 * d1));
+            double med;
+            {
+#pragma clang fp contract(off)
+                med = (F & 1) ? (double)v1 : ((double)v0 + (double)v1) / 2.0;
+            }
+            if (lane < 5) {
+                const double o = lane == 0 ? mean : lane == 1 ? sqrt(qq / (double)F) : lane == 2 ? (double)mx
+                                 : lane == 3 ? (double)mn : med;
+                featb[5 * q + lane] = (float)o;
+            }
+        }
+    } else {  // long sequences: partial ranks over all waves, then one wave per sequence
+        rank_partial([&](int q, int j) { return q == 2 ? (float)c.fZ[j] : (q == 0 ? c.fE[j] : c.fM[j]); },
+                     3, F, c.rank, wid, lane);
+        __syncthreads();
+        for (int t = tid; t < 3 * F; t += NT) {
+            const int q = t / F, e = t - q * F;
+            const int r = c.rank[t];
+            const double val = q == 2 ? (double)c.fZ[e] : (double)(q == 0 ? c.fE[e] : c.fM[e]);
+            if (r == r0) sh->oslo[q] = val;
+            if (r == r1) sh->oshi[q] = val;
+        }
+        __syncthreads();
+        if (wid < 3) {
+            double s = 0.0, mx = -INFINITY, mn = INFINITY;
+            for (int q = lane; q < F; q += 64) {
+                const double x = wid == 0 ? (double)c.fE[q] : wid == 1 ? (double)c.fM[q] : (double)c.fZ[q];
+                s += x;
+                mx = fmax(mx, x);
+                mn = fmin(mn, x);
+            }
+            s = wave_sum(s);
+            mx = wave_maxd(mx);
+            mn = wave_mind(mn);
+            const double mean = s / (double)F;
+            double qq = 0.0;
+            for (int q = lane; q < F; q += 64) {
+                const double x = wid == 0 ? (double)c.fE[q] : wid == 1 ? (double)c.fM[q] : (double)c.fZ[q];
+                const double d = x - mean;
+                qq = fma(d, d, qq);
+            }
+            qq = wave_sum(qq);
+            double med;
+            {
+#pragma clang fp contract(off)
+                med = (F & 1) ? sh->oshi[wid] : (sh->oslo[wid] + sh->oshi[wid]) / 2.0;
+            }
+            if (lane < 5) {
+                const double o = lane == 0 ? mean : lane == 1 ? sqrt(qq / (double)F) : lane == 2 ? mx
+                                 : lane == 3 ? mn : med;
+                featb[5 * wid + lane] = (float)o;
             }
         }
     }
-    __syncthreads();
     STAMP(i, 9);
-    if (wid < 3 && !SKIP(32)) {
-        double s = 0.0, mx = -INFINITY, mn = INFINITY;
-        for (int q = lane; q < F; q += 64) {
-            const double x = wid == 0 ? (double)c.fE[q] : wid == 1 ? (double)c.fM[q] : (double)c.fZ[q];
-            s += x;
-            mx = fmax(mx, x);
-            mn = fmin(mn, x);
-        }
-        s = wave_sum(s);
-        mx = wave_maxd(mx);
-        mn = wave_mind(mn);
-        const double mean = s / (double)F;
-        double qq = 0.0;
-        for (int q = lane; q < F; q += 64) {
-            const double x = wid == 0 ? (double)c.fE[q] : wid == 1 ? (double)c.fM[q] : (double)c.fZ[q];
-            const double d = x - mean;
-            qq = fma(d, d, qq);
-        }
-        qq = wave_sum(qq);
-        double med;
-        {
-#pragma clang fp contract(off)
-            med = (F & 1) ? sh->oshi[wid] : (sh->oslo[wid] + sh->oshi[wid]) / 2.0;
-        }
-        if (lane < 5) {
-            const double o = lane == 0 ? mean : lane == 1 ? sqrt(qq / (double)F) : lane == 2 ? mx
-                             : lane == 3 ? mn : med;
-            featb[5 * wid + lane] = (float)o;
-        }
-    }
     if (p.seq)
         for (int g = tid; g < F && g < p.ld_seq; g += NT) {
             float *o = p.seq + ((size_t)i * p.ld_seq + g) * 3;

@@ -22,8 +22,12 @@ def t(mask, reps=30):
     for _ in range(reps): fx(x)
     b.record(); torch.cuda.synchronize()
     return a.elapsed_time(b) / reps * 1e3
-names = {0: "none", 1: "vad frames", 2: "p90", 4: "scan", 8: "R4", 16: "R5 ranks", 32: "R5 stats",
-         64: "R2 bits", 128: "R1 stats", 1 | 2 | 4: "all VAD", 8 | 16 | 32: "R4+R5", 255: "everything"}
+names = {0: "none", 4: "scan", 4 | 2: "scan+p90", 4 | 2 | 1: "scan+p90+vad frames", 8: "R4",
+         16: "R5 ranks", 32: "R5 stats", 16 | 32: "R5", 64: "R2 bits", 8 | 16 | 32: "R4+R5",
+         255 & ~128: "all but R1", 255: "everything"}
+if "--once" in sys.argv:  # one configuration (DSP_SKIP) for PMC collection
+    t(int(os.environ.get("DSP_SKIP", "0")), reps=5)
+    sys.exit(0)
 base = t(0)
 res = {"base_us": round(base, 2)}
 for m, nm in names.items():
