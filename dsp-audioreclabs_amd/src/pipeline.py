@@ -28,7 +28,7 @@ def _as_device(x, dtype, device):
     import torch
     if isinstance(x, torch.Tensor):
         return x.to(device=device, dtype=dtype).contiguous()
-    return torch.as_tensor(np.ascontiguousarray(x)).to(device=device, dtype=dtype).contiguous()
+    return torch.as_tensor(np.array(x, copy=True, order="C")).to(device=device, dtype=dtype).contiguous()
 
 
 class FeatureExtractor:
