@@ -33,6 +33,23 @@
 #include "dsp_audiorec.h"
 #include "extract_layout.h"
 
+// implementation switches (A/B timing builds: tools/ab.sh)
+#ifndef DSP_P90PAR
+#define DSP_P90PAR 0  // p90: rank ranges over all waves (else: bitonic sort in wave 0; faster)
+#endif
+#ifndef DSP_R5SPLIT
+#define DSP_R5SPLIT 1  // R5: medians and moments on separate waves
+#endif
+#ifndef DSP_IW1
+#define DSP_IW1 0  // word loads from one address when inside the clip (measured slower)
+#endif
+#ifndef DSP_NEAR0
+#define DSP_NEAR0 1  // R4: one packed subtraction of fl(mq) when |t0| <= 2
+#endif
+#ifndef DSP_CVARG
+#define DSP_CVARG 1  // LDS layout as a kernel argument
+#endif
+
 namespace dsp {
 
 static constexpr int NT = EXTRACT_THREADS;
@@ -71,6 +88,8 @@ struct ExtractParams {
     int ld_seq;
     unsigned long long *stamps;  // diagnostic build only (else null)
     int skip;                    // diagnostic build only: phases to skip (timing ablation)
+    ExtractCarve cv;             // LDS layout, computed on the host (kernel arguments can be
+                                 // re-read instead of being held in registers)
 };
 
 typedef short short8 __attribute__((ext_vector_type(8)));
@@ -340,6 +359,8 @@ struct Ctx {
     float *fE, *fM;
     int32_t *fZ;
     int *rank;  // rank scratch: nvcap or 3 * fcap ints
+    int *pS1;   // partial-word moments at the two ends of each VAD frame (2 * nvcap)
+    unsigned long long *pS2;
     int *defer;
     int64_t total;
     int stamp_clip;  // clip index for the diagnostic stamps
@@ -357,8 +378,14 @@ __device__ __forceinline__ short8 load_vec(const ExtractParams &p, const ClipRef
 __device__ __forceinline__ void issue_word(short8 *q, const ExtractParams &p, const ClipRef &c, int w)
 {
     const short8 *src = reinterpret_cast<const short8 *>(p.pcm + c.base);
+    if (DSP_IW1 && 4 * w + 3 < c.nvec) {  // one address, immediate offsets
+        const short8 *a = src + 4 * w;
 #pragma unroll
-    for (int k = 0; k < 4; k++) q[k] = src[min(4 * w + k, c.nvec - 1)];
+        for (int k = 0; k < 4; k++) q[k] = a[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) q[k] = src[min(4 * w + k, c.nvec - 1)];
+    }
 }
 
 __device__ __forceinline__ short2v half_pair(const short8 &x, int i)
@@ -392,6 +419,26 @@ __device__ __forceinline__ int chg_count(const uint32_t *posw, int x0, int x1, i
         }
     }
     return c;
+}
+// set change bits in buffer-bit range [x0, x1), one lane walking the words in order (each
+// positive-bit word is read once)
+__device__ __forceinline__ int chg_run(const uint32_t *posw, int x0, int x1)
+{
+    if (x1 <= x0) return 0;
+    const int w0 = x0 >> 5, w1 = (x1 - 1) >> 5;
+    uint32_t a = posw[w0];
+    int cnt = 0;
+#pragma unroll 4
+    for (int w = w0; w <= w1; w++) {
+        const uint32_t b = posw[w + 1];
+        cnt += __popc(a ^ ((a >> 1) | (b << 31)));
+        a = b;
+    }
+    // remove the bits below x0 and from x1 on
+    const uint32_t c0 = chg_word(posw, w0), c1 = chg_word(posw, w1);
+    cnt -= __popc(c0 & ((1u << (x0 & 31)) - 1u));
+    if (x1 & 31) cnt -= __popc(c1 & (~0u << (x1 & 31)));
+    return cnt;
 }
 __device__ __forceinline__ int pos_bit(const uint32_t *posw, int u) { return (posw[u >> 5] >> (u & 31)) & 1; }
 
@@ -749,7 +796,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     STAMP(i, 0);
 
     // ---- R1: integer sum / min / max; exact moments per 32-sample word -----------------------
-    long long K = 0;
+    int K = 0;  // <= RREG * 32 * 32768 per thread (longer clips: one word per loop trip)
     int kmin_s = 0x7fffffff, kmax_s = -0x7fffffff - 1;
     short2v pmin = {32767, 32767}, pmax = {-32768, -32768};
     auto r1_word = [&](const short8 *q, int w) {
@@ -808,7 +855,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     {
         const int kmn = min(kmin_s, min((int)pmin.x, (int)pmin.y));
         const int kmx = max(kmax_s, max((int)pmax.x, (int)pmax.y));
-        const long long ks = wave_sum(K);
+        const long long ks = (long long)wave_sum(K);  // <= 64 threads' sums < 2^31
         const int wmn = wave_min(kmn), wmx = wave_max(kmx);
         if (lane == 0) {
             sh->red_k[wid] = ks;
@@ -833,7 +880,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     const int tpos = (int)floor(mq) + 1;
     const int t0 = (int)floor(mq + 0.5);
     const float deltaf = (float)(mq - (double)t0);  // mq - t0 is exact (Sterbenz)
-    const float invMf = Mp > 0.0 ? (float)(1.0 / Mp) : 0.0f;
+    const float invMf = Mp > 0.0 ? __builtin_amdgcn_rcpf((float)Mp) : 0.0f;  // scale only: 1 ulp
     const int nv = (p.do_vad && n >= L) ? (n - L) / S + 1 : 0;
     STAMP(i, 1);
 
@@ -883,63 +930,80 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     int st = 0, en = n;
     if (nv > 0) {
         // frame f = buffer samples [u0, u0 + L): exact moments from the word sums plus the two
-        // partial words (re-read from L2), sign changes from the bits; one quad per frame
+        // partial words at its ends, sign changes from the bits.
+        // Pass A, one thread per frame end: the partial word's moments (re-read from L2).
+        if (!EXACT && !SKIP(1)) {
+            for (int t = tid; t < 2 * nv; t += NT) {
+                const int f = t >> 1;
+                const bool end = t & 1;
+                const int u0 = lead + f * S, u1 = u0 + L;
+                const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
+                int pw = -1, e0 = 0, e1 = 0;
+                if (!end && (u0 & 31)) {
+                    pw = wa;
+                    e0 = u0 & 31;
+                    e1 = min(32, u1 - 32 * wa);
+                } else if (end && (u1 & 31) && (wb != wa || !(u0 & 31))) {
+                    pw = wb;
+                    e0 = max(0, u0 - 32 * wb);
+                    e1 = u1 & 31;
+                }
+                int t1 = 0;
+                unsigned long long t2 = 0;
+                if (pw >= 0) {
+                    short8 q[4];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) q[k] = load_vec(p, cur, min(4 * pw + k, cur.nvec - 1));
+#pragma unroll 1
+                    for (int k = 0; k < 4; k++) {
+                        const short8 v = k == 0 ? q[0] : k == 1 ? q[1] : k == 2 ? q[2] : q[3];
+#pragma unroll
+                        for (int e = 0; e < 8; e++) {
+                            const int x = v[e];
+                            const int ee = 8 * k + e;
+                            if (ee >= e0 && ee < e1) {
+                                t1 += x;
+                                t2 += (unsigned)(x * x);
+                            }
+                        }
+                    }
+                }
+                c.pS1[t] = t1;
+                c.pS2[t] = t2;
+            }
+            __syncthreads();
+        }
+        // Pass B, one quad per frame: interior word sums and sign changes, each lane a
+        // contiguous quarter
         const int q4 = tid >> 2, lq = tid & 3;
         for (int f0 = 0; f0 < nv; f0 += NT / 4) {
             const int f = f0 + q4;
             const bool act = f < nv;
-            long long s1 = 0;
+            int s1 = 0;  // |frame sum| <= L * 32768 < 2^31 for L < 65536
             unsigned long long s2 = 0;
             int zc = 0;
             if (act && !SKIP(1)) {
                 const int u0 = lead + f * S, u1 = u0 + L;
                 if (!EXACT) {
                     const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
-                    // the partial words at the frame's ends: lane 0 the first, lane 1 the last;
-                    // their loads go out before the LDS sums so the L2 latency overlaps them
-                    int pw = -1, e0 = 0, e1 = 0;
-                    if (lq == 0 && (u0 & 31)) {
-                        pw = wa;
-                        e0 = u0 & 31;
-                        e1 = min(32, u1 - 32 * wa);
-                    } else if (lq == 1 && (u1 & 31) && (wb != wa || !(u0 & 31))) {
-                        pw = wb;
-                        e0 = max(0, u0 - 32 * wb);
-                        e1 = u1 & 31;
-                    }
-                    short8 q[4];
-                    const int lw = pw >= 0 ? pw : wa;
-#pragma unroll
-                    for (int k = 0; k < 4; k++) q[k] = load_vec(p, cur, min(4 * lw + k, cur.nvec - 1));
                     const int wi0 = (u0 & 31) ? wa + 1 : wa, wi1 = (u1 & 31) ? wb - 1 : wb;
+                    const int per = (wi1 - wi0 + 4) >> 2;
+                    const int ws = wi0 + lq * per, we = min(ws + per - 1, wi1);
 #pragma unroll 3
-                    for (int w = wi0 + lq; w <= wi1; w += 4) {
+                    for (int w = ws; w <= we; w++) {
                         s1 += c.wS1[w];
                         s2 += c.wS2[w];
                     }
-                    if (pw >= 0) {
-                        int t1 = 0;
-                        unsigned long long t2 = 0;
-#pragma unroll 1
-                        for (int k = 0; k < 4; k++) {
-                            const short8 v = k == 0 ? q[0] : k == 1 ? q[1] : k == 2 ? q[2] : q[3];
-#pragma unroll
-                            for (int e = 0; e < 8; e++) {
-                                const int x = v[e];
-                                const int ee = 8 * k + e;
-                                if (ee >= e0 && ee < e1) {
-                                    t1 += x;
-                                    t2 += (unsigned)(x * x);
-                                }
-                            }
-                        }
-                        s1 += t1;
-                        s2 += t2;
+                    if (lq == 0) {
+                        s1 += c.pS1[2 * f] + c.pS1[2 * f + 1];
+                        s2 += c.pS2[2 * f] + c.pS2[2 * f + 1];
                     }
                 }
-                zc = chg_count(c.posw, u0, u1 - 1, lq, 4);
+                const int np_ = L - 1, pq = (np_ + 3) >> 2;  // pairs [u0, u1 - 1) in quarters
+                const int x0 = u0 + min(lq * pq, np_), x1 = u0 + min((lq + 1) * pq, np_);
+                zc = chg_run(c.posw, x0, x1);
             }
-            s1 = dpp_quad_sum_i64(s1);
+            s1 = dpp_quad_reduce(s1, OpAdd());
             s2 = dpp_quad_sum64(s2);
             zc = dpp_quad_reduce(zc, OpAdd());
             if (act && lq == 0) {
@@ -963,7 +1027,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
             }
             if (SKIP(2)) {
                 if (tid == 0) sh->pa = sh->pb = c.vE[r0];
-            } else if (nv <= 128) {  // wave 0: bitonic sort of the energies, then the scan below
+            } else if (nv <= 128 && !DSP_P90PAR) {  // wave 0: bitonic sort of the energies
                 if (wid == 0) {
                     unsigned long long a[2];
                     a[0] = lane < nv ? dkey(c.vE[lane]) : ~0ull;
@@ -973,6 +1037,21 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                     if (lane == 0) {
                         sh->pa = pa;
                         sh->pb = pb;
+                    }
+                }
+            } else if (nv <= 128) {
+                // order-preserving keys in registers (lane + 64h); wave w takes candidates w,
+                // w + 8, ...: #{keys below} and #{equal keys} by two ballots per half give the
+                // ranks the candidate's value occupies (ties are equal values: no index needed)
+                const unsigned long long k0 = lane < nv ? dkey(c.vE[lane]) : ~0ull;
+                const unsigned long long k1 = lane + 64 < nv ? dkey(c.vE[lane + 64]) : ~0ull;
+                for (int i2 = wid; i2 < nv; i2 += NWAVE) {
+                    const unsigned long long e = lane_read(i2 < 64 ? k0 : k1, i2 & 63);
+                    const int lt = __popcll(__ballot(k0 < e)) + __popcll(__ballot(k1 < e));
+                    const int eq = __popcll(__ballot(k0 == e)) + __popcll(__ballot(k1 == e));
+                    if (lane == 0) {
+                        if (r0 >= lt && r0 < lt + eq) sh->pa = dkey_value(e);
+                        if (r1 >= lt && r1 < lt + eq) sh->pb = dkey_value(e);
                     }
                 }
             } else if (nv <= 256) {
@@ -987,7 +1066,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                 }
             }
         }
-        if (nv > 128 || SKIP(2)) __syncthreads();  // (wave 0 alone wrote pa / pb otherwise)
+        __syncthreads();
         STAMP(i, 3);
         if (SKIP(4)) {
             if (tid == 0) {
@@ -1031,16 +1110,23 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     const int wrow = EXTRACT_WROW(L);
     typedef float float2v __attribute__((ext_vector_type(2)));
     const float2v mt = {-t0f, -t0f}, md = {-deltaf, -deltaf};
-    auto frame_vec = [&](auto padded_t, const short8 &x8, const float *wr, int jb, int lim, float2v &ea,
-                         float &ma, float &mb) {
-        constexpr bool PADDED = decltype(padded_t)::value;
+    // |t0| <= 2: x = k - fl(mq) in one packed add (|error| <= 2^-22, i.e. < 1e-6 of any nonzero
+    // |x| of an integer signal); otherwise (k - t0) exactly, then - delta
+    const bool near0 = t0 >= -2 && t0 <= 2;
+    const float2v mqf = {(float)-mq, (float)-mq};
+    auto frame_vec = [&](auto padded_t, auto near_t, const short8 &x8, const float *wr, int jb, int lim,
+                         float2v &ea, float &ma, float &mb) {
+        constexpr bool PADDED = decltype(padded_t)::value, NEAR0 = decltype(near_t)::value;
         const float4 wa = *reinterpret_cast<const float4 *>(wr + jb);
         const float4 wb = *reinterpret_cast<const float4 *>(wr + jb + 4);
         const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
 #pragma unroll
         for (int h = 0; h < 4; h++) {
             float2v x = {(float)x8[2 * h], (float)x8[2 * h + 1]};
-            x = (x + mt) + md;  // (k - t0) exact, then - delta
+            if (NEAR0)
+                x = x + mqf;
+            else
+                x = (x + mt) + md;  // (k - t0) exact, then - delta
             float2v w = {wv[2 * h], wv[2 * h + 1]};
             if (PADDED) {  // samples past the crop are zero padding
                 const int j = jb + 2 * h;  // window index of the pair's first sample
@@ -1075,17 +1161,19 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
             short8 xv[R4_KV];
 #pragma unroll
             for (int k = 0; k < R4_KV; k++) xv[k] = load_vec(p, cur, min(v0 + rl + 16 * k, vmax));
-            auto run = [&](auto pt) {
+            auto run = [&](auto pt, auto nt) {
 #pragma unroll
                 for (int k = 0; k < R4_KV; k++) {
                     const int v = v0 + rl + 16 * k;
-                    if (v <= vb) frame_vec(pt, xv[k], wr, 8 * v - u0, lim, ea, ma, mb);
+                    if (v <= vb) frame_vec(pt, nt, xv[k], wr, 8 * v - u0, lim, ea, ma, mb);
                 }
             };
             if (padded)
-                run(BoolT<true>());
+                run(BoolT<true>(), BoolT<false>());
+            else if (DSP_NEAR0 && near0)
+                run(BoolT<false>(), BoolT<true>());
             else
-                run(BoolT<false>());
+                run(BoolT<false>(), BoolT<false>());
         }
         const float E1 = dpp_row_reduce(ea.x + ea.y, OpAdd()) * sE;
         const float M1 = dpp_row_reduce(ma + mb, OpAdd()) * sM;
@@ -1115,38 +1203,43 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
         // wave q alone handles sequence q (E, M, ZCR): lanes hold v[lane], v[lane + 64]; the
         // order statistics by ballot ranks over readlane'd candidates, then mean / std (fp64 sums)
         // and max / min -- no barrier
-        if (wid < 3 && !SKIP(48)) {
-            const int q = wid;
+        if (wid < (DSP_R5SPLIT ? 6 : 3) && !SKIP(48)) {
+            const int q = wid % 3;
             auto get = [&](int j) -> float { return q == 0 ? c.fE[j] : q == 1 ? c.fM[j] : (float)c.fZ[j]; };
             const bool in0 = lane < F, in1 = lane + 64 < F;
             const float x0 = in0 ? get(lane) : 0.f, x1 = in1 ? get(lane + 64) : 0.f;
-            unsigned a[2] = {in0 ? fkey(x0) : ~0u, in1 ? fkey(x1) : ~0u};
-            float v0, v1;
-            if (F <= 64) {
-                unsigned b[1] = {a[0]};
-                wave_bitonic<1>(b, lane);
-                v0 = fkey_value(sorted_at<1>(b, r0));
-                v1 = fkey_value(sorted_at<1>(b, r1));
-            } else {
-                wave_bitonic<2>(a, lane);
-                v0 = fkey_value(sorted_at<2>(a, r0));
-                v1 = fkey_value(sorted_at<2>(a, r1));
-            }
-            const double s = wave_sum((in0 ? (double)x0 : 0.0) + (in1 ? (double)x1 : 0.0));
-            const float mx = wave_reduce(fmaxf(in0 ? x0 : -INFINITY, in1 ? x1 : -INFINITY), OpMax());
-            const float mn = wave_reduce(fminf(in0 ? x0 : INFINITY, in1 ? x1 : INFINITY), OpMin());
-            const double mean = s / (double)F;
-            const double d0 = in0 ? (double)x0 - mean : 0.0, d1 = in1 ? (double)x1 - mean : 0.0;
-            const double qq = wave_sum(fma(d0, d0, d1 * d1));
-            double med;
-            {
+            if (wid < 3 || !DSP_R5SPLIT) {  // median by an in-wave bitonic sort
+                unsigned a[2] = {in0 ? fkey(x0) : ~0u, in1 ? fkey(x1) : ~0u};
+                float v0, v1;
+                if (F <= 64) {
+                    unsigned b[1] = {a[0]};
+                    wave_bitonic<1>(b, lane);
+                    v0 = fkey_value(sorted_at<1>(b, r0));
+                    v1 = fkey_value(sorted_at<1>(b, r1));
+                } else {
+                    wave_bitonic<2>(a, lane);
+                    v0 = fkey_value(sorted_at<2>(a, r0));
+                    v1 = fkey_value(sorted_at<2>(a, r1));
+                }
+                double med;
+                {
 #pragma clang fp contract(off)
-                med = (F & 1) ? (double)v1 : ((double)v0 + (double)v1) / 2.0;
+                    med = (F & 1) ? (double)v1 : ((double)v0 + (double)v1) / 2.0;
+                }
+                if (lane == 0) featb[5 * q + 4] = (float)med;
             }
-            if (lane < 5) {
-                const double o = lane == 0 ? mean : lane == 1 ? sqrt(qq / (double)F) : lane == 2 ? (double)mx
-                                 : lane == 3 ? (double)mn : med;
-                featb[5 * q + lane] = (float)o;
+            if (wid >= 3 || !DSP_R5SPLIT) {  // mean, population std (fp64 sums), max, min
+                const double s = wave_sum((in0 ? (double)x0 : 0.0) + (in1 ? (double)x1 : 0.0));
+                const float mx = wave_reduce(fmaxf(in0 ? x0 : -INFINITY, in1 ? x1 : -INFINITY), OpMax());
+                const float mn = wave_reduce(fminf(in0 ? x0 : INFINITY, in1 ? x1 : INFINITY), OpMin());
+                const double mean = s / (double)F;
+                const double d0 = in0 ? (double)x0 - mean : 0.0, d1 = in1 ? (double)x1 - mean : 0.0;
+                const double qq = wave_sum(fma(d0, d0, d1 * d1));
+                if (lane < 4) {
+                    const double o = lane == 0 ? mean : lane == 1 ? sqrt(qq / (double)F) : lane == 2 ? (double)mx
+                                     : (double)mn;
+                    featb[5 * q + lane] = (float)o;
+                }
             }
         }
     } else {  // long sequences: partial ranks over all waves, then one wave per sequence
@@ -1230,7 +1323,11 @@ __device__ __forceinline__ void issue_clip(short8 (&regs)[NRV], const ExtractPar
 
 __device__ __forceinline__ Ctx make_ctx(const ExtractParams &p, unsigned char *lds)
 {
+#if DSP_CVARG
+    const ExtractCarve &cv = p.cv;
+#else
     const ExtractCarve cv = extract_carve(p.ncap, p.L, p.S, EXTRACT_DEFER_CAP);
+#endif
     Ctx c;
     c.sh = reinterpret_cast<Shared *>(lds + cv.sh);
     c.wtab = reinterpret_cast<const float *>(lds + cv.wtab);
@@ -1243,6 +1340,8 @@ __device__ __forceinline__ Ctx make_ctx(const ExtractParams &p, unsigned char *l
     c.fM = reinterpret_cast<float *>(lds + cv.fM);
     c.fZ = reinterpret_cast<int32_t *>(lds + cv.fZ);
     c.rank = reinterpret_cast<int *>(lds + cv.rank);
+    c.pS1 = reinterpret_cast<int *>(lds + cv.pS1);
+    c.pS2 = reinterpret_cast<unsigned long long *>(lds + cv.pS2);
     c.defer = reinterpret_cast<int *>(lds + cv.defer);
     c.total = 0;
     c.stamp_clip = 0;
@@ -1266,8 +1365,11 @@ __device__ __attribute__((noinline)) void clip_exact(const ExtractParams p, int 
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void extract_kernel(ExtractParams p)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const ExtractCarve cv = extract_carve(p.ncap, p.L, p.S, EXTRACT_DEFER_CAP);
-    float *wt = reinterpret_cast<float *>(lds + cv.wtab);
+#if DSP_CVARG
+    float *wt = reinterpret_cast<float *>(lds + p.cv.wtab);
+#else
+    float *wt = reinterpret_cast<float *>(lds + extract_carve(p.ncap, p.L, p.S, EXTRACT_DEFER_CAP).wtab);
+#endif
     Ctx c = make_ctx(p, lds);
     Shared *sh = c.sh;
 
@@ -1283,9 +1385,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void ex
     }
     __syncthreads();
     const int wrow = EXTRACT_WROW(L);
-    for (int m = tid; m < 4 * wrow; m += NT) {
-        const int r = m / wrow, j = m - r * wrow - EXTRACT_WPAD - r;
-        wt[m] = (j >= 0 && j < L) ? (float)p.window[j] : 0.f;
+    for (int j = tid - EXTRACT_WPAD - 3; j < wrow - EXTRACT_WPAD; j += NT) {  // one load per weight
+        const float w = (j >= 0 && j < L) ? (float)p.window[j] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int m = j + EXTRACT_WPAD + r;  // copy r holds w[m - WPAD - r] at m
+            if (m >= 0 && m < wrow) wt[r * wrow + m] = w;
+        }
     }
     for (int q0 = wid * 64; q0 < L; q0 += NT) {
         const int j = q0 + lane;
@@ -1403,6 +1509,7 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     p.seq = seq;
     p.ld_seq = ld_seq;
     p.stamps = (unsigned long long *)g_stamp_buffer;
+    p.cv = extract_carve((int)max_len, frame_length, frame_shift, EXTRACT_DEFER_CAP);
     p.skip = g_skip;
     // persistent grid: two workgroups per CU when their LDS fits (one otherwise), each walking
     // clips blockIdx, blockIdx + grid, ...

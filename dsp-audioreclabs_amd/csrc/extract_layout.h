@@ -20,7 +20,7 @@
 #define EXTRACT_WROW(L) ((((L) + 2 * EXTRACT_WPAD + 4) + 3) & ~3)
 
 struct ExtractCarve {
-    int sh, wtab, posw, wS2, wS1, vE, vZ, fE, fM, fZ, rank, defer, total;
+    int sh, wtab, posw, wS2, wS1, vE, vZ, fE, fM, fZ, rank, pS2, pS1, defer, total;
     int nvcap, fcap, nwmax;
 };
 
@@ -48,6 +48,8 @@ __host__ __device__ inline ExtractCarve extract_carve(int ncap, int L, int S, in
     DSP_TAKE(fM, 4 * c.fcap);
     DSP_TAKE(fZ, 4 * c.fcap);
     DSP_TAKE(rank, 4 * (c.nvcap > 3 * c.fcap ? c.nvcap : 3 * c.fcap));
+    DSP_TAKE(pS2, 16 * c.nvcap);  // partial-word moments at the two ends of each VAD frame
+    DSP_TAKE(pS1, 8 * c.nvcap);
     DSP_TAKE(defer, 4 * per_wg);
 #undef DSP_TAKE
     c.total = o;
