@@ -1,7 +1,9 @@
-# A/B timing of library variants on one box: tools/ab.sh name1 name2 ... (lib/libdsp_audiorec_<name>.so; "base" = default)
+# A/B timing on one box: tools/ab.sh spec ...   spec = lib name (lib/libdsp_audiorec_<name>.so, "base" =
+# default lib) optionally with :v3 / :v4 to force the kernel variant
 for rep in 1 2; do
-for v in "$@"; do
+for spec in "$@"; do
+  v=${spec%%:*}; var=${spec#*:}; [ "$var" = "$spec" ] && var=""
   lib=$PWD/dsp-audioreclabs_amd/lib/libdsp_audiorec_$v.so; [ "$v" = base ] && lib=$PWD/dsp-audioreclabs_amd/lib/libdsp_audiorec.so
-  DSP_LIB_PATH=$lib DIAG_VARIANTS=vad_hamming timeout -k 10 100 python tools/diag_extract.py 1000 | grep '"ms"' | sed "s/^/$v /"
+  DSP_EXTRACT_VARIANT=$var DSP_LIB_PATH=$lib DIAG_VARIANTS=vad_hamming,novad_hamming timeout -k 10 100 python tools/diag_extract.py 1000 | grep '"ms"' | tr -d '\n' | sed "s/^/$spec /"; echo
 done
 done
