@@ -62,10 +62,29 @@ static constexpr int NRV = 4 * RREG;       // 16-B vectors per thread in registe
 // pointer is a kernel argument (SGPRs), so a stamp never waits on a memory load.
 #define STAMP(clip, k)                                                                           \
     do {                                                                                         \
-        if (threadIdx.x == 0 && p.stamps) p.stamps[(size_t)(clip) * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+        if (threadIdx.x == 0 && p.stamps) p.stamps[(size_t)(clip) * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 #define SKIP(bit) ((p.skip & (bit)) != 0)  // phase ablation for timing (outputs are garbage)
+// per workgroup (row blockIdx.x, slots 16..): real-time and shader-clock stamps (WG_STAMP, at
+// entry and exit) and shader-clock stamps inside the prologue (WG_CK)
+#define WG_STAMP(k)                                                                          \
+    do {                                                                                     \
+        if (threadIdx.x == 0 && p.stamps) {                                                  \
+            p.stamps[(size_t)blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memrealtime();      \
+            p.stamps[(size_t)blockIdx.x * 32 + (k) + 1] = __builtin_amdgcn_s_memtime();      \
+        }                                                                                    \
+    } while (0)
+#define WG_CK(k)                                                                             \
+    do {                                                                                     \
+        if (threadIdx.x == 0 && p.stamps) p.stamps[(size_t)blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 #else
+#define WG_STAMP(k) \
+    do {            \
+    } while (0)
+#define WG_CK(k) \
+    do {         \
+    } while (0)
 #define STAMP(clip, k) \
     do {               \
     } while (0)
@@ -1375,35 +1394,49 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void ex
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int L = p.L, G = gridDim.x;
+    WG_STAMP(16);
 
-    // window (create_window, :278-296) -> LDS once as four shifted zero-padded fp32 copies; its
-    // support [j0, j1] by ballots
+    // window (create_window, :278-296) -> LDS once as four shifted zero-padded fp32 copies, and
+    // its support [j0, j1] by ballots: every weight read is issued before the first use, so the
+    // prologue costs one L2 round trip (windows longer than WPRE * NT loop over the rest).
+    constexpr int WPRE = 3;
+    double wv[WPRE];
+#pragma unroll
+    for (int k = 0; k < WPRE; k++) {
+        const int j = tid + NT * k;
+        wv[k] = j < L ? p.window[j] : 0.0;
+    }
+    WG_CK(18);
     if (tid == 0) {
         sh->j0 = L;
         sh->j1 = -1;
         sh->ndefer = 0;
     }
-    __syncthreads();
     const int wrow = EXTRACT_WROW(L);
-    for (int j = tid - EXTRACT_WPAD - 3; j < wrow - EXTRACT_WPAD; j += NT) {  // one load per weight
-        const float w = (j >= 0 && j < L) ? (float)p.window[j] : 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int m = j + EXTRACT_WPAD + r;  // copy r holds w[m - WPAD - r] at m
-            if (m >= 0 && m < wrow) wt[r * wrow + m] = w;
-        }
+    for (int t = tid; t < 4 * (wrow - L); t += NT) {  // zero pads: m < WPAD + r, m >= L + WPAD + r
+        const int r = t / (wrow - L), q = t - r * (wrow - L);
+        wt[r * wrow + (q < EXTRACT_WPAD + r ? q : q + L)] = 0.f;
     }
-    for (int q0 = wid * 64; q0 < L; q0 += NT) {
+    __syncthreads();
+    WG_CK(19);
+    auto put_weight = [&](int q0, double w) {  // weight j = q0 + lane (q0 wave-uniform)
         const int j = q0 + lane;
         const bool in = j < L;
-        const double w = in ? p.window[j] : 0.0;
+        if (in) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) wt[r * wrow + j + EXTRACT_WPAD + r] = (float)w;
+        }
         const unsigned long long m = __ballot(in && w > 0.0);
         if (lane == 0 && m) {
             atomicMin(&sh->j0, q0 + __ffsll((long long)m) - 1);
             atomicMax(&sh->j1, q0 + 63 - __clzll((long long)m));
         }
-    }
+    };
+#pragma unroll
+    for (int k = 0; k < WPRE; k++) put_weight(NT * k + wid * 64, wv[k]);
+    for (int q0 = NT * WPRE + wid * 64; q0 < L; q0 += NT) put_weight(q0, q0 + lane < L ? p.window[q0 + lane] : 0.0);
     __syncthreads();
+    WG_CK(20);
 
     short8 regs[NRV];
     for (int i = blockIdx.x; i < p.B; i += G) {
@@ -1432,6 +1465,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void ex
         clip_exact(p, j);
         __syncthreads();
     }
+    WG_STAMP(22);
 }
 
 }  // namespace dsp

@@ -22,7 +22,7 @@ if STAMPS:
     import ctypes
     from src import _hip
     L_ = _hip.load_library()
-    stamp_buf = torch.zeros((C, 16), dtype=torch.int64, device="cuda")
+    stamp_buf = torch.zeros((C, 32), dtype=torch.int64, device="cuda")
     L_.dsp_debug_set_stamp_buffer.argtypes = [ctypes.c_void_p]
     assert L_.dsp_debug_set_stamp_buffer(ctypes.c_void_p(stamp_buf.data_ptr())) == 0
 x = torch.as_tensor(make_batch(C, base_seed=0)).cuda()
@@ -40,6 +40,10 @@ for name, kw in [("vad_hamming", dict(window_type="hamming", do_endpoint_detecti
     if STAMPS:
         stamp_buf.zero_(); fx(x); torch.cuda.synchronize()
         st_ = stamp_buf.cpu().numpy().astype(np.float64)
+        if os.environ.get("DIAG_SAVE"):
+            np.save(os.environ["DIAG_SAVE"] + "_" + name + ".npy", stamp_buf.cpu().numpy())
+            np.save(os.environ["DIAG_SAVE"] + "_" + name + "_nframes.npy", out["n_frames"].cpu().numpy())
+            np.save(os.environ["DIAG_SAVE"] + "_" + name + "_se.npy", out["start_end"].cpu().numpy())
         ph = {}
         # stamp ids in program order and the phase each one ends
         seq = [0, 1, 2, 7, 8, 3, 10, 11, 4, 5, 9, 6]
@@ -58,6 +62,15 @@ for name, kw in [("vad_hamming", dict(window_type="hamming", do_endpoint_detecti
             ph["period"] = float(np.median(st_[G:2 * G, 0] - st_[:G, 0]))
         span = (st_[:, 6].max() - st_[:, 0].min())
         ph["grid_span_cycles"] = float(span)
+        wg = st_[:, 16] > 0
+        if wg.any():
+            rt0, ck0, rt1, ck1 = (st_[wg, k] for k in (16, 17, 22, 23))
+            ph["clock_ghz_median"] = float(np.median((ck1 - ck0) / (rt1 - rt0) * 0.1))
+            ph["wg_us_median"] = float(np.median(rt1 - rt0) / 100.0)
+            ph["wg_us_max"] = float((rt1 - rt0).max() / 100.0)
+            ph["start_skew_us"] = float((rt0.max() - rt0.min()) / 100.0)
+            ph["end_first_last_us"] = [float((rt1.min() - rt0.min()) / 100.0), float((rt1.max() - rt0.min()) / 100.0)]
+            ph["n_wg"] = int(wg.sum())
     res[name] = dict(ms=ms, flagged=int(((st >> 8) & 1).sum()), errors=int((st & 0xFF).astype(bool).sum()),
                      n_frames_mean=float(out["n_frames"].float().mean().item()))
     if STAMPS: res[name]["phase_cycles_median"] = ph

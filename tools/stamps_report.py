@@ -1,0 +1,26 @@
+"""Summarise a raw stamp dump of tools/diag_extract.py (DIAG_SAVE): prologue, per-phase and
+per-workgroup times in microseconds.  usage: stamps_report.py raw.npy [clock_ghz]"""
+import sys
+import numpy as np
+st = np.load(sys.argv[1]).astype(np.float64)
+G = int((st[:, 16] > 0).sum())
+rt0, ck0, rt1, ck1 = (st[:G, k] for k in (16, 17, 22, 23))
+ghz = np.median((ck1 - ck0) / (rt1 - rt0) * 0.1)
+cyc = ghz * 1e3
+C = len(st)
+print("workgroups %d  clock %.3f GHz" % (G, ghz))
+dur = (rt1 - rt0) / 100
+print("wg us  p0 %.2f p50 %.2f p90 %.2f max %.2f" % tuple(np.percentile(dur, [0, 50, 90, 100])))
+print("prologue us  p50 %.2f max %.2f" % (np.median((st[:G, 0] - ck0) / cyc), ((st[:G, 0] - ck0) / cyc).max()))
+for k, nm in ((18, "window loads issued"), (19, "pads + barrier"), (20, "weights + barrier"), (0, "first clip issued")):
+    print("  prologue %-20s p50 %.2f" % (nm, np.median((st[:G, k] - ck0) / cyc)))
+tot = (st[:, 6] - st[:, 0]) / cyc
+print("clip us  p50 %.2f p90 %.2f | first round p50 %.2f (wg<%d %.2f, wg>=%d %.2f) later %.2f" % (
+    np.median(tot), np.percentile(tot, 90), np.median(tot[:G]), G // 2, np.median(tot[:G // 2]), G // 2,
+    np.median(tot[G // 2:G]), np.median(tot[G:]) if C > G else 0))
+names = {1: "R1 load+stats", 2: "R2 pos", 8: "VAD frames", 3: "p90", 10: "noise+thr", 11: "scan",
+         4: "vad out", 5: "R4", 9: "R5 medians", 6: "R5 stats"}
+seq = [0, 1, 2, 8, 3, 10, 11, 4, 5, 9, 6]
+for a, b in zip(seq, seq[1:]):
+    d = (st[:, b] - st[:, a]) / cyc
+    print("  %-14s p50 %.2f  oldWG %.2f newWG %.2f" % (names[b], np.median(d), np.median(d[:G // 2]), np.median(d[G // 2:G])))
