@@ -1046,13 +1046,38 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
             }
             if (SKIP(2)) {
                 if (tid == 0) sh->pa = sh->pb = c.vE[r0];
-            } else if (nv <= 128 && !DSP_P90PAR) {  // wave 0: bitonic sort of the energies
+            } else if (nv <= 128 && !DSP_P90PAR) {
+                // wave 0: bitonic sort of the high halves of the order-preserving keys; the rank's
+                // element is the one holding that high half, or, when several do, the one of the
+                // right rank among them by the full key
                 if (wid == 0) {
-                    unsigned long long a[2];
-                    a[0] = lane < nv ? dkey(c.vE[lane]) : ~0ull;
-                    a[1] = lane + 64 < nv ? dkey(c.vE[lane + 64]) : ~0ull;
+                    const unsigned long long f0 = lane < nv ? dkey(c.vE[lane]) : ~0ull;
+                    const unsigned long long f1 = lane + 64 < nv ? dkey(c.vE[lane + 64]) : ~0ull;
+                    const unsigned h0 = (unsigned)(f0 >> 32), h1 = (unsigned)(f1 >> 32);
+                    unsigned a[2] = {h0, h1};
                     wave_bitonic<2>(a, lane);
-                    const double pa = dkey_value(sorted_at<2>(a, r0)), pb = dkey_value(sorted_at<2>(a, r1));
+                    auto full_at = [&](int r) -> double {
+                        const unsigned kh = sorted_at<2>(a, r);  // never the pad's ~0u: r < nv
+                        const unsigned long long c0 = __ballot(h0 == kh), c1 = __ballot(h1 == kh);
+                        if (__popcll(c0) + __popcll(c1) == 1)
+                            return dkey_value(c0 ? lane_read(f0, __ffsll((long long)c0) - 1)
+                                                 : lane_read(f1, __ffsll((long long)c1) - 1));
+                        const int rr = r - (__popcll(__ballot(h0 < kh)) + __popcll(__ballot(h1 < kh)));
+                        unsigned long long res = 0;
+                        for (int hh = 0; hh < 2; hh++) {
+                            unsigned long long cm = hh ? c1 : c0;
+                            while (cm) {
+                                const int l = __ffsll((long long)cm) - 1;
+                                cm &= cm - 1;
+                                const unsigned long long e = lane_read(hh ? f1 : f0, l);
+                                const int lt = __popcll(__ballot(h0 == kh && f0 < e)) + __popcll(__ballot(h1 == kh && f1 < e));
+                                const int eq = __popcll(__ballot(f0 == e)) + __popcll(__ballot(f1 == e));
+                                if (rr >= lt && rr < lt + eq) res = e;
+                            }
+                        }
+                        return dkey_value(res);
+                    };
+                    const double pa = full_at(r0), pb = full_at(r1);
                     if (lane == 0) {
                         sh->pa = pa;
                         sh->pb = pb;
@@ -1381,7 +1406,10 @@ __device__ __attribute__((noinline)) void clip_exact(const ExtractParams p, int 
 }
 
 // 128 VGPRs: two 512-thread workgroups per CU
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void extract_kernel(ExtractParams p)
+#ifndef EXTRACT_WAVES_PER_EU
+#define EXTRACT_WAVES_PER_EU 4
+#endif
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVES_PER_EU))) void extract_kernel(ExtractParams p)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 #if DSP_CVARG

@@ -8,8 +8,12 @@
 #ifndef DSP_EXTRACT_LAYOUT_H
 #define DSP_EXTRACT_LAYOUT_H
 
+#ifndef EXTRACT_THREADS
 #define EXTRACT_THREADS 512
+#endif
+#ifndef EXTRACT_RREG
 #define EXTRACT_RREG 3                   // 32-sample words per thread held in registers
+#endif
 #define EXTRACT_LDS_LIMIT (160 * 1024)   // one CU
 #define EXTRACT_LDS_SHARED (80 * 1024)   // per workgroup when two share a CU
 #define EXTRACT_DEFER_CAP 256            // near-tie clips one workgroup can redo exactly

@@ -139,3 +139,38 @@ def test_unpadded_buffer_tail():
             assert out["n_frames"][1] == r["n_frames"]
             assert np.array_equal(out["seq"][1, :r["n_frames"], 2], r["seq"][:, 2]), (n, lead, vad)
             assert not feat_close(out["feat"][1], r["feat"]).any()
+
+
+def test_tied_vad_energies():
+    """p90 selection with tied endpoint energies: a signal periodic in the hop gives every full
+    VAD frame the same energy (all keys equal); +-1 perturbations of single samples give
+    energies that differ only in their low bits (equal high key halves)."""
+    import torch
+    from src.pipeline import FeatureExtractor, create_window
+    L, S, n = 1102, 441, 44100
+    t = np.arange(n)
+    base = (8000 * np.sin(2 * np.pi * t / 147.0)).astype(np.int16)  # period 147 divides S
+    clips = [base.copy()]
+    c = base.copy()
+    for f in range(10, 90, 3):  # one sample per frame, +-1: relative energy change ~1e-7
+        c[f * S + 500] += 1 if f % 2 else -1
+    clips.append(c)
+    c = base.copy()
+    c[: 20 * S] //= 50  # quiet lead-in: a crop with tied loud frames
+    clips.append(c)
+    c = clips[1].copy()
+    c[: 20 * S] //= 50
+    clips.append(c)
+    off = np.arange(len(clips) + 1, dtype=np.int64) * n
+    pcm = np.concatenate(clips + [np.zeros(8, np.int16)])
+    fx = FeatureExtractor(L, S, "hamming", True, return_vad_lists=True)
+    out = {k: v.cpu().numpy() for k, v in fx(torch.as_tensor(pcm).cuda(), off).items()}
+    w = create_window("hamming", L)
+    for i, c in enumerate(clips):
+        r = oracle.process_clip(c, L, S, w, do_vad=True)
+        assert (out["status"][i] & 0xFF) == r["status"] == 0
+        assert tuple(out["start_end"][i]) == (r["start"], r["end"]), i
+        assert out["n_frames"][i] == r["n_frames"], i
+        nv = len(r["vad_energy"])
+        np.testing.assert_allclose(out["vad_energy"][i, :nv], r["vad_energy"], rtol=1e-12, atol=0)
+        assert not feat_close(out["feat"][i], r["feat"]).any(), i
