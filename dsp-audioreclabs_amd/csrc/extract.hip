@@ -46,9 +46,6 @@
 #ifndef DSP_NEAR0
 #define DSP_NEAR0 1  // R4: one packed subtraction of fl(mq) when |t0| <= 2
 #endif
-#ifndef DSP_CVARG
-#define DSP_CVARG 1  // LDS layout as a kernel argument
-#endif
 
 namespace dsp {
 
@@ -501,7 +498,7 @@ __device__ __forceinline__ bool bits_any_in(const BitsK<KC> &m, int lo, int hi) 
 // Double-threshold endpoint scan (src/audio_processing.py:186-273) by wave 0 on vE/vZ with the
 // p90 order statistics in sh->pa / sh->pb.  Writes sh->n3 (-1: no high-energy frame), n1, n6;
 // returns the near-tie flag.
-template <bool CERTIFY>
+template <bool CERTIFY, bool FAST>
 __device__ __forceinline__ int vad_scan(const ExtractParams &p, const Ctx &c, int nv, int lane)
 {
     const double *vE = c.vE;
@@ -577,7 +574,7 @@ __device__ __forceinline__ int vad_scan(const ExtractParams &p, const Ctx &c, in
             n6 = b6 >= 0 ? b6 - 1 : nv - 1;
         }
     };
-    if (nv <= 128) {
+    if (FAST || nv <= 128) {
         short_scan(IntT<2>());
     } else if (nv <= 256) {
         short_scan(IntT<4>());
@@ -802,7 +799,9 @@ __device__ __forceinline__ void ballot_select(Get get, int n, int r0, int r1, do
 // r * NT + tid in regs[4r .. 4r+3]).  EXACT = false: endpoint energies from exact moments,
 // decisions certified; returns false on a near tie (the clip is then redone with EXACT = true
 // after the persistent loop).
-template <bool EXACT>
+// FAST: the compile-time LDS layout (extract_carve_fast); the clip is in registers and there are
+// at most 128 VAD and feature frames, so the long-clip paths drop out
+template <bool EXACT, bool FAST>
 __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, int i, const ClipRef &cur,
                                           short8 (&regs)[NRV])
 {
@@ -856,7 +855,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     };
     // clips of up to RREG * NT words stream from the registers loaded before this call; longer
     // ones are read word by word here and again in R2 (the second read hits L2)
-    const bool inreg = nword <= RREG * NT;
+    const bool inreg = FAST || nword <= RREG * NT;
     if (inreg) {
 #pragma unroll
         for (int r = 0; r < RREG; r++) {
@@ -1046,7 +1045,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
             }
             if (SKIP(2)) {
                 if (tid == 0) sh->pa = sh->pb = c.vE[r0];
-            } else if (nv <= 128 && !DSP_P90PAR) {
+            } else if ((FAST || nv <= 128) && !DSP_P90PAR) {
                 // wave 0: bitonic sort of the high halves of the order-preserving keys; the rank's
                 // element is the one holding that high half, or, when several do, the one of the
                 // right rank among them by the full key
@@ -1120,7 +1119,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                 sh->exact = 0;
             }
         } else if (wid == 0) {
-            const int flag = vad_scan<!EXACT>(p, c, nv, lane);
+            const int flag = vad_scan<!EXACT, FAST>(p, c, nv, lane);
             if (lane == 0) sh->exact = (!EXACT && Mp > 0.0) ? flag : 0;
         }
         __syncthreads();
@@ -1235,7 +1234,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
             c.fZ[g] = z;
         }
     }
-    if (F > 128)
+    if (!FAST && F > 128)
         for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
     __syncthreads();
     STAMP(i, 5);
@@ -1243,7 +1242,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     // ---- R5: 15-d statistics (compute_statistics x 3, fe.py:46-62) ------------------------
     // np.median: the middle order statistic (odd F) or the mean of the two middle ones
     const int r0 = (F - 1) / 2, r1 = F / 2;
-    if (F <= 128) {
+    if (FAST || F <= 128) {
         // wave q alone handles sequence q (E, M, ZCR): lanes hold v[lane], v[lane + 64]; the
         // order statistics by ballot ranks over readlane'd candidates, then mean / std (fp64 sums)
         // and max / min -- no barrier
@@ -1365,13 +1364,8 @@ __device__ __forceinline__ void issue_clip(short8 (&regs)[NRV], const ExtractPar
     for (int r = 0; r < RREG; r++) issue_word(&regs[4 * r], p, c, r * NT + (int)threadIdx.x);
 }
 
-__device__ __forceinline__ Ctx make_ctx(const ExtractParams &p, unsigned char *lds)
+__device__ __forceinline__ Ctx ctx_from(const ExtractCarve &cv, unsigned char *lds)
 {
-#if DSP_CVARG
-    const ExtractCarve &cv = p.cv;
-#else
-    const ExtractCarve cv = extract_carve(p.ncap, p.L, p.S, EXTRACT_DEFER_CAP);
-#endif
     Ctx c;
     c.sh = reinterpret_cast<Shared *>(lds + cv.sh);
     c.wtab = reinterpret_cast<const float *>(lds + cv.wtab);
@@ -1391,33 +1385,41 @@ __device__ __forceinline__ Ctx make_ctx(const ExtractParams &p, unsigned char *l
     c.stamp_clip = 0;
     return c;
 }
+template <bool FAST>
+__device__ __forceinline__ Ctx make_ctx(const ExtractParams &p, unsigned char *lds)
+{
+    if constexpr (FAST) {
+        constexpr ExtractCarve cv = extract_carve_fast();
+        return ctx_from(cv, lds);
+    } else {
+        return ctx_from(p.cv, lds);
+    }
+}
 
 // the rare near-tie redo, compiled out of line so its exact-order machinery does not weigh on
 // the register allocation of the streaming path
+template <bool FAST>
 __device__ __attribute__((noinline)) void clip_exact(const ExtractParams p, int i)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    Ctx c = make_ctx(p, lds);
+    Ctx c = make_ctx<FAST>(p, lds);
     c.stamp_clip = i;
     const ClipRef cr = clip_ref(p, i);
     short8 regs[NRV];
     issue_clip(regs, p, cr);
-    clip_body<true>(p, c, i, cr, regs);
+    clip_body<true, FAST>(p, c, i, cr, regs);
 }
 
 // 128 VGPRs: two 512-thread workgroups per CU
 #ifndef EXTRACT_WAVES_PER_EU
 #define EXTRACT_WAVES_PER_EU 4
 #endif
+template <bool FAST>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVES_PER_EU))) void extract_kernel(ExtractParams p)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-#if DSP_CVARG
-    float *wt = reinterpret_cast<float *>(lds + p.cv.wtab);
-#else
-    float *wt = reinterpret_cast<float *>(lds + extract_carve(p.ncap, p.L, p.S, EXTRACT_DEFER_CAP).wtab);
-#endif
-    Ctx c = make_ctx(p, lds);
+    Ctx c = make_ctx<FAST>(p, lds);
+    float *wt = const_cast<float *>(c.wtab);
     Shared *sh = c.sh;
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1475,7 +1477,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
         }
         issue_clip(regs, p, cur);
         c.stamp_clip = i;
-        const bool done = clip_body<false>(p, c, i, cur, regs);
+        const bool done = clip_body<false, FAST>(p, c, i, cur, regs);
         if (!done && tid == 0) {
             if (sh->ndefer < EXTRACT_DEFER_CAP) {
                 c.defer[sh->ndefer++] = i;
@@ -1490,7 +1492,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     const int nd = sh->ndefer;
     for (int d = 0; d < nd; d++) {
         const int j = c.defer[d];
-        clip_exact(p, j);
+        clip_exact<FAST>(p, j);
         __syncthreads();
     }
     WG_STAMP(22);
@@ -1546,7 +1548,9 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
         if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
             return DSP_ERR_HIP;
         g_num_cus = prop.multiProcessorCount;
-        (void)hipFuncSetAttribute((const void *)dsp::extract_kernel,
+        (void)hipFuncSetAttribute((const void *)dsp::extract_kernel<true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
+        (void)hipFuncSetAttribute((const void *)dsp::extract_kernel<false>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
     }
     dsp::ExtractParams p;
@@ -1574,11 +1578,16 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     p.cv = extract_carve((int)max_len, frame_length, frame_shift, EXTRACT_DEFER_CAP);
     p.skip = g_skip;
     // persistent grid: two workgroups per CU when their LDS fits (one otherwise), each walking
-    // clips blockIdx, blockIdx + grid, ...
-    const int per_cu = lds <= EXTRACT_LDS_SHARED ? 2 : 1;
+    // clips blockIdx, blockIdx + grid, ...; the compile-time layout whenever the launch fits it
+    const bool fast = extract_fast_fits((int)max_len, frame_length, frame_shift);
+    const size_t lds_launch = fast ? (size_t)extract_carve_fast().total : lds;
+    const int per_cu = lds_launch <= EXTRACT_LDS_SHARED ? 2 : 1;
     const int slots = per_cu * g_num_cus;
     const int grid = B < slots ? B : slots;
-    hipLaunchKernelGGL(dsp::extract_kernel, dim3(grid), dim3(dsp::NT), lds, (hipStream_t)stream, p);
+    if (fast)
+        hipLaunchKernelGGL(dsp::extract_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch, (hipStream_t)stream, p);
+    else
+        hipLaunchKernelGGL(dsp::extract_kernel<false>, dim3(grid), dim3(dsp::NT), lds_launch, (hipStream_t)stream, p);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? DSP_OK : DSP_ERR_HIP + (int)e;
 }

@@ -28,21 +28,22 @@ struct ExtractCarve {
     int nvcap, fcap, nwmax;
 };
 
-// ncap = longest clip of the launch (samples)
-__host__ __device__ inline ExtractCarve extract_carve(int ncap, int L, int S, int per_wg)
+// Region offsets from the capacities: nwmax 32-sample words (incl. the alignment lead), nvcap VAD
+// frames, fcap feature frames, wrow floats per shifted window copy, per_wg deferred clips.
+__host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvcap, int fcap, int wrow, int per_wg)
 {
-    ExtractCarve c;
+    ExtractCarve c{};
     int o = 0;
 #define DSP_TAKE(field, bytes)             \
     do {                                   \
         c.field = o;                       \
         o = (o + (int)(bytes) + 15) & ~15; \
     } while (0)
-    c.nvcap = ncap >= L ? (ncap - L) / S + 1 : 0;
-    c.fcap = ncap <= L ? 1 : (ncap - L + S - 1) / S + 1;
-    c.nwmax = (ncap + 7 + 31) / 32 + 1;  // 32-sample words incl. the alignment lead
+    c.nvcap = nvcap;
+    c.fcap = fcap;
+    c.nwmax = nwmax;
     DSP_TAKE(sh, EXTRACT_SHARED_BYTES);
-    DSP_TAKE(wtab, 16 * EXTRACT_WROW(L));          // 4 zero-padded copies of w, shifted by 0..3
+    DSP_TAKE(wtab, 16 * wrow);                   // 4 zero-padded copies of w, shifted by 0..3
     DSP_TAKE(posw, 4 * (c.nwmax + 2));           // positive-sample bits (+2 zero sentinels)
     DSP_TAKE(wS2, 8 * c.nwmax);                  // per word: sum k^2 (exact, u64)
     DSP_TAKE(wS1, 4 * c.nwmax);                  // per word: sum k
@@ -58,6 +59,34 @@ __host__ __device__ inline ExtractCarve extract_carve(int ncap, int L, int S, in
 #undef DSP_TAKE
     c.total = o;
     return c;
+}
+
+// ncap = longest clip of the launch (samples)
+__host__ __device__ inline ExtractCarve extract_carve(int ncap, int L, int S, int per_wg)
+{
+    const int nvcap = ncap >= L ? (ncap - L) / S + 1 : 0;
+    const int fcap = ncap <= L ? 1 : (ncap - L + S - 1) / S + 1;
+    const int nwmax = (ncap + 7 + 31) / 32 + 1;
+    return extract_carve_caps(nwmax, nvcap, fcap, EXTRACT_WROW(L), per_wg);
+}
+
+// The fast kernel's layout is fixed at compile time (every LDS address an immediate) and serves
+// every launch whose clips fit it: the whole clip in registers, <= 128 VAD and feature frames,
+// window rows of <= EXTRACT_FAST_WROW floats (frame_length <= 1256).
+#define EXTRACT_FAST_NV 128
+#define EXTRACT_FAST_NF 128
+#define EXTRACT_FAST_WROW 1280
+#define EXTRACT_FAST_NWORD (EXTRACT_THREADS * EXTRACT_RREG)
+__host__ __device__ constexpr ExtractCarve extract_carve_fast()
+{
+    return extract_carve_caps(EXTRACT_FAST_NWORD + 1, EXTRACT_FAST_NV, EXTRACT_FAST_NF, EXTRACT_FAST_WROW,
+                              EXTRACT_DEFER_CAP);
+}
+__host__ __device__ inline bool extract_fast_fits(int ncap, int L, int S)
+{
+    const ExtractCarve c = extract_carve(ncap, L, S, EXTRACT_DEFER_CAP);
+    return (ncap + 7 + 31) / 32 <= EXTRACT_FAST_NWORD && c.nvcap <= EXTRACT_FAST_NV &&
+           c.fcap <= EXTRACT_FAST_NF && EXTRACT_WROW(L) <= EXTRACT_FAST_WROW;
 }
 
 #endif

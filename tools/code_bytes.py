@@ -8,6 +8,7 @@ src_path = os.path.join(CS, "extract.hip")
 flags = ["-O3", "--offload-arch=gfx950", "-std=c++17", "-I" + os.path.join(R, "include"), "-Wno-unused-function",
          "--offload-device-only", "-gline-tables-only"] + sys.argv[1:]
 hip = "/opt/rocm/bin/hipcc"
+KSEL = os.environ.get("KSEL", "extract_kernelILb1E")  # the fast instantiation
 subprocess.run([hip] + flags + ["-S", src_path, "-o", "/tmp/cb.s"], check=True, stderr=subprocess.DEVNULL)
 subprocess.run([hip] + flags + ["-c", src_path, "-o", "/tmp/cb.o"], check=True, stderr=subprocess.DEVNULL)
 obj = "/tmp/cb.o"
@@ -30,7 +31,7 @@ ins = []
 infn = False
 for l in dis.split("\n"):
     m = re.match(r"^[0-9a-f]+ <(\S+)>:", l)
-    if m: infn = "extract_kernel" in m.group(1); continue
+    if m: infn = KSEL in m.group(1); continue
     m = re.match(r"\s+(\S+).*//\s*([0-9A-F]+):((?:\s[0-9A-F]{8})+)", l)
     if infn and m: ins.append((m.group(1), 4 * len(m.group(3).split())))
 # .s: (mnemonic, phase) of extract_kernel
@@ -46,7 +47,7 @@ for l in open("/tmp/cb.s").read().split("\n"):
         inside = [x for x in chain if body[0] <= x <= body[1]]
         if inside: cur = inside[0]
         elif chain and chain[0] > 0: cur = chain[0]
-    if fn and "extract_kernel" in fn and re.match(r"\s+[vsdgb][a-z0-9_]+(\s|$)", l) and not l.strip().startswith((".", ";")):
+    if fn and KSEL in fn and re.match(r"\s+[vsdgb][a-z0-9_]+(\s|$)", l) and not l.strip().startswith((".", ";")):
         sins.append((l.split()[0], phase(cur) if cur else "pre"))
 n = min(len(ins), len(sins))
 mism = sum(1 for a, b in zip(ins, sins) if a[0] != b[0])
