@@ -43,6 +43,12 @@
 #ifndef DSP_IW1
 #define DSP_IW1 0  // word loads from one address when inside the clip (measured slower)
 #endif
+#ifndef DSP_ASM_ABS
+#define DSP_ASM_ABS 1  // R4: M += |y| as one VOP3 add with the abs modifier
+#endif
+#ifndef DSP_ASM_SQ2
+#define DSP_ASM_SQ2 1  // R1: k^2 pair sums as VOP3 v_dot2 with an inline zero
+#endif
 #ifndef DSP_NEAR0
 #define DSP_NEAR0 1  // R4: one packed subtraction of fl(mq) when |t0| <= 2
 #endif
@@ -62,6 +68,9 @@ static constexpr int NRV = 4 * RREG;       // 16-B vectors per thread in registe
         if (threadIdx.x == 0 && p.stamps) p.stamps[(size_t)(clip) * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 #define SKIP(bit) ((p.skip & (bit)) != 0)  // phase ablation for timing (outputs are garbage)
+// phase doubling (skip bits 8..): the phase runs twice; it is idempotent, so results and the
+// control flow after it are unchanged and the extra time / instructions are the phase's own
+#define REPS(bit) ((p.skip & ((bit) << 8)) ? 2 : 1)
 // per workgroup (row blockIdx.x, slots 16..): real-time and shader-clock stamps (WG_STAMP, at
 // entry and exit) and shader-clock stamps inside the prologue (WG_CK)
 #define WG_STAMP(k)                                                                          \
@@ -86,6 +95,7 @@ static constexpr int NRV = 4 * RREG;       // 16-B vectors per thread in registe
     do {               \
     } while (0)
 #define SKIP(bit) false
+#define REPS(bit) 1
 #endif
 
 struct ExtractParams {
@@ -402,6 +412,30 @@ __device__ __forceinline__ void issue_word(short8 *q, const ExtractParams &p, co
 #pragma unroll
         for (int k = 0; k < 4; k++) q[k] = src[min(4 * w + k, c.nvec - 1)];
     }
+}
+
+// acc + |v| in one VOP3 add with the abs source modifier
+__device__ __forceinline__ float add_abs(float acc, float v)
+{
+#if DSP_ASM_ABS
+    float r;
+    asm("v_add_f32_e64 %0, |%1|, %2" : "=v"(r) : "v"(v), "v"(acc));
+    return r;
+#else
+    return acc + fabsf(v);
+#endif
+}
+// k0^2 + k1^2 of a sample pair in one VOP3 v_dot2 with an inline-zero accumulator (the builtin
+// becomes v_mov 0 + v_dot2c)
+__device__ __forceinline__ int sq2(short2v d)
+{
+#if DSP_ASM_SQ2
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %1, 0" : "=v"(r) : "v"(d));
+    return r;
+#else
+    return __builtin_amdgcn_sdot2(d, d, 0, false);
+#endif
 }
 
 __device__ __forceinline__ short2v half_pair(const short8 &x, int i)
@@ -830,7 +864,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                     pmin = __builtin_elementwise_min(pmin, d);
                     pmax = __builtin_elementwise_max(pmax, d);
                     s1 = __builtin_amdgcn_sdot2(d, ones, s1, false);
-                    s2 += (unsigned)__builtin_amdgcn_sdot2(d, d, 0, false);  // <= 2^31: unsigned
+                    s2 += (unsigned)sq2(d);  // <= 2^31: unsigned
                 }
         } else {  // first / last word of the clip: real samples only
 #pragma unroll 1
@@ -856,29 +890,40 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     // clips of up to RREG * NT words stream from the registers loaded before this call; longer
     // ones are read word by word here and again in R2 (the second read hits L2)
     const bool inreg = FAST || nword <= RREG * NT;
-    if (inreg) {
+    for (int rep_ = 0; rep_ < REPS(1); rep_++) {  // diagnostic doubling (REPS)
+        if (rep_) {
 #pragma unroll
-        for (int r = 0; r < RREG; r++) {
-            const int w = r * NT + tid;
-            if (w < nword && !SKIP(128)) r1_word(&regs[4 * r], w);
+            for (int k = 0; k < NRV; k++) asm volatile("" : "+v"(regs[k]));  // no hoisting
+            K = 0;
+            kmin_s = 0x7fffffff;
+            kmax_s = -0x7fffffff - 1;
+            pmin = (short2v){32767, 32767};
+            pmax = (short2v){-32768, -32768};
         }
-    } else {
+        if (inreg) {
+#pragma unroll
+            for (int r = 0; r < RREG; r++) {
+                const int w = r * NT + tid;
+                if (w < nword && !SKIP(128)) r1_word(&regs[4 * r], w);
+            }
+        } else {
 #pragma unroll 1
-        for (int w = tid; w < nword; w += NT) {
-            short8 q[4];
-            issue_word(q, p, cur, w);
-            r1_word(q, w);
+            for (int w = tid; w < nword; w += NT) {
+                short8 q[4];
+                issue_word(q, p, cur, w);
+                r1_word(q, w);
+            }
         }
-    }
-    {
-        const int kmn = min(kmin_s, min((int)pmin.x, (int)pmin.y));
-        const int kmx = max(kmax_s, max((int)pmax.x, (int)pmax.y));
-        const long long ks = (long long)wave_sum(K);  // <= 64 threads' sums < 2^31
-        const int wmn = wave_min(kmn), wmx = wave_max(kmx);
-        if (lane == 0) {
-            sh->red_k[wid] = ks;
-            sh->red_a[wid] = wmn;
-            sh->red_b[wid] = wmx;
+        {
+            const int kmn = min(kmin_s, min((int)pmin.x, (int)pmin.y));
+            const int kmx = max(kmax_s, max((int)pmax.x, (int)pmax.y));
+            const long long ks = (long long)wave_sum(K);  // <= 64 threads' sums < 2^31
+            const int wmn = wave_min(kmn), wmx = wave_max(kmx);
+            if (lane == 0) {
+                sh->red_k[wid] = ks;
+                sh->red_a[wid] = wmn;
+                sh->red_b[wid] = wmx;
+            }
         }
     }
     __syncthreads();
@@ -926,18 +971,23 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
         }
         c.posw[w] = P;
     };
-    if (inreg) {
+    for (int rep_ = 0; rep_ < REPS(2); rep_++) {  // diagnostic doubling (REPS)
+        if (rep_)
 #pragma unroll
-        for (int r = 0; r < RREG; r++) {
-            const int w = r * NT + tid;
-            if (w < nword && !SKIP(64)) r2_word(&regs[4 * r], w);
-        }
-    } else {
+            for (int k = 0; k < NRV; k++) asm volatile("" : "+v"(regs[k]));  // no hoisting
+        if (inreg) {
+#pragma unroll
+            for (int r = 0; r < RREG; r++) {
+                const int w = r * NT + tid;
+                if (w < nword && !SKIP(64)) r2_word(&regs[4 * r], w);
+            }
+        } else {
 #pragma unroll 1
-        for (int w = tid; w < nword; w += NT) {
-            short8 q[4];
-            issue_word(q, p, cur, w);
-            r2_word(q, w);
+            for (int w = tid; w < nword; w += NT) {
+                short8 q[4];
+                issue_word(q, p, cur, w);
+                r2_word(q, w);
+            }
         }
     }
     if (tid < 2) c.posw[nword + tid] = 0;
@@ -950,179 +1000,186 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
         // frame f = buffer samples [u0, u0 + L): exact moments from the word sums plus the two
         // partial words at its ends, sign changes from the bits.
         // Pass A, one thread per frame end: the partial word's moments (re-read from L2).
-        if (!EXACT && !SKIP(1)) {
-            for (int t = tid; t < 2 * nv; t += NT) {
-                const int f = t >> 1;
-                const bool end = t & 1;
-                const int u0 = lead + f * S, u1 = u0 + L;
-                const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
-                int pw = -1, e0 = 0, e1 = 0;
-                if (!end && (u0 & 31)) {
-                    pw = wa;
-                    e0 = u0 & 31;
-                    e1 = min(32, u1 - 32 * wa);
-                } else if (end && (u1 & 31) && (wb != wa || !(u0 & 31))) {
-                    pw = wb;
-                    e0 = max(0, u0 - 32 * wb);
-                    e1 = u1 & 31;
-                }
-                int t1 = 0;
-                unsigned long long t2 = 0;
-                if (pw >= 0) {
-                    short8 q[4];
+        for (int rep_ = 0; rep_ < REPS(4); rep_++) {  // diagnostic doubling (REPS)
+            if (!EXACT && !SKIP(1)) {
+                for (int repa_ = 0; repa_ < REPS(128); repa_++)  // diagnostic doubling (REPS)
+                for (int t = tid; t < 2 * nv; t += NT) {
+                    const int f = t >> 1;
+                    const bool end = t & 1;
+                    const int u0 = lead + f * S, u1 = u0 + L;
+                    const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
+                    int pw = -1, e0 = 0, e1 = 0;
+                    if (!end && (u0 & 31)) {
+                        pw = wa;
+                        e0 = u0 & 31;
+                        e1 = min(32, u1 - 32 * wa);
+                    } else if (end && (u1 & 31) && (wb != wa || !(u0 & 31))) {
+                        pw = wb;
+                        e0 = max(0, u0 - 32 * wb);
+                        e1 = u1 & 31;
+                    }
+                    int t1 = 0;
+                    unsigned long long t2 = 0;
+                    if (pw >= 0) {
+                        short8 q[4];
 #pragma unroll
-                    for (int k = 0; k < 4; k++) q[k] = load_vec(p, cur, min(4 * pw + k, cur.nvec - 1));
+                        for (int k = 0; k < 4; k++) q[k] = load_vec(p, cur, min(4 * pw + k, cur.nvec - 1));
 #pragma unroll 1
-                    for (int k = 0; k < 4; k++) {
-                        const short8 v = k == 0 ? q[0] : k == 1 ? q[1] : k == 2 ? q[2] : q[3];
+                        for (int k = 0; k < 4; k++) {
+                            const short8 v = k == 0 ? q[0] : k == 1 ? q[1] : k == 2 ? q[2] : q[3];
 #pragma unroll
-                        for (int e = 0; e < 8; e++) {
-                            const int x = v[e];
-                            const int ee = 8 * k + e;
-                            if (ee >= e0 && ee < e1) {
-                                t1 += x;
-                                t2 += (unsigned)(x * x);
+                            for (int e = 0; e < 8; e++) {
+                                const int x = v[e];
+                                const int ee = 8 * k + e;
+                                if (ee >= e0 && ee < e1) {
+                                    t1 += x;
+                                    t2 += (unsigned)(x * x);
+                                }
                             }
                         }
                     }
+                    c.pS1[t] = t1;
+                    c.pS2[t] = t2;
                 }
-                c.pS1[t] = t1;
-                c.pS2[t] = t2;
+                __syncthreads();
+            }
+            // Pass B, one quad per frame: interior word sums and sign changes, each lane a
+            // contiguous quarter
+            const int q4 = tid >> 2, lq = tid & 3;
+            for (int f0 = 0; f0 < nv; f0 += NT / 4) {
+                const int f = f0 + q4;
+                const bool act = f < nv;
+                int s1 = 0;  // |frame sum| <= L * 32768 < 2^31 for L < 65536
+                unsigned long long s2 = 0;
+                int zc = 0;
+                if (act && !SKIP(1)) {
+                    const int u0 = lead + f * S, u1 = u0 + L;
+                    if (!EXACT) {
+                        const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
+                        const int wi0 = (u0 & 31) ? wa + 1 : wa, wi1 = (u1 & 31) ? wb - 1 : wb;
+                        const int per = (wi1 - wi0 + 4) >> 2;
+                        const int ws = wi0 + lq * per, we = min(ws + per - 1, wi1);
+#pragma unroll 3
+                        for (int w = ws; w <= we; w++) {
+                            s1 += c.wS1[w];
+                            s2 += c.wS2[w];
+                        }
+                        if (lq == 0) {
+                            s1 += c.pS1[2 * f] + c.pS1[2 * f + 1];
+                            s2 += c.pS2[2 * f] + c.pS2[2 * f + 1];
+                        }
+                    }
+                    const int np_ = L - 1, pq = (np_ + 3) >> 2;  // pairs [u0, u1 - 1) in quarters
+                    const int x0 = u0 + min(lq * pq, np_), x1 = u0 + min((lq + 1) * pq, np_);
+                    zc = chg_run(c.posw, x0, x1);
+                }
+                s1 = dpp_quad_reduce(s1, OpAdd());
+                s2 = dpp_quad_sum64(s2);
+                zc = dpp_quad_reduce(zc, OpAdd());
+                if (act && lq == 0) {
+                    c.rank[f] = 0;
+                    c.vE[f] = EXACT ? np_energy_exact(clip_g, f * S, L, mq, Mp)
+                                    : energy_from_moments(s2, s1, L, mq, Mp);
+                    c.vZ[f] = zc;
+                }
             }
             __syncthreads();
         }
-        // Pass B, one quad per frame: interior word sums and sign changes, each lane a
-        // contiguous quarter
-        const int q4 = tid >> 2, lq = tid & 3;
-        for (int f0 = 0; f0 < nv; f0 += NT / 4) {
-            const int f = f0 + q4;
-            const bool act = f < nv;
-            int s1 = 0;  // |frame sum| <= L * 32768 < 2^31 for L < 65536
-            unsigned long long s2 = 0;
-            int zc = 0;
-            if (act && !SKIP(1)) {
-                const int u0 = lead + f * S, u1 = u0 + L;
-                if (!EXACT) {
-                    const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
-                    const int wi0 = (u0 & 31) ? wa + 1 : wa, wi1 = (u1 & 31) ? wb - 1 : wb;
-                    const int per = (wi1 - wi0 + 4) >> 2;
-                    const int ws = wi0 + lq * per, we = min(ws + per - 1, wi1);
-#pragma unroll 3
-                    for (int w = ws; w <= we; w++) {
-                        s1 += c.wS1[w];
-                        s2 += c.wS2[w];
-                    }
-                    if (lq == 0) {
-                        s1 += c.pS1[2 * f] + c.pS1[2 * f + 1];
-                        s2 += c.pS2[2 * f] + c.pS2[2 * f + 1];
-                    }
-                }
-                const int np_ = L - 1, pq = (np_ + 3) >> 2;  // pairs [u0, u1 - 1) in quarters
-                const int x0 = u0 + min(lq * pq, np_), x1 = u0 + min((lq + 1) * pq, np_);
-                zc = chg_run(c.posw, x0, x1);
-            }
-            s1 = dpp_quad_reduce(s1, OpAdd());
-            s2 = dpp_quad_sum64(s2);
-            zc = dpp_quad_reduce(zc, OpAdd());
-            if (act && lq == 0) {
-                c.rank[f] = 0;
-                c.vE[f] = EXACT ? np_energy_exact(clip_g, f * S, L, mq, Mp)
-                                : energy_from_moments(s2, s1, L, mq, Mp);
-                c.vZ[f] = zc;
-            }
-        }
-        __syncthreads();
         STAMP(i, 8);
-        // p90 order statistics (:198) by parallel ranks
-        {
-            const double vi = (double)(nv - 1) * 0.9;
-            int r0, r1;
-            if (vi >= (double)(nv - 1)) {
-                r0 = r1 = nv - 1;
-            } else {
-                r0 = (int)floor(vi);
-                r1 = r0 + 1;
-            }
-            if (SKIP(2)) {
-                if (tid == 0) sh->pa = sh->pb = c.vE[r0];
-            } else if ((FAST || nv <= 128) && !DSP_P90PAR) {
-                // wave 0: bitonic sort of the high halves of the order-preserving keys; the rank's
-                // element is the one holding that high half, or, when several do, the one of the
-                // right rank among them by the full key
-                if (wid == 0) {
-                    const unsigned long long f0 = lane < nv ? dkey(c.vE[lane]) : ~0ull;
-                    const unsigned long long f1 = lane + 64 < nv ? dkey(c.vE[lane + 64]) : ~0ull;
-                    const unsigned h0 = (unsigned)(f0 >> 32), h1 = (unsigned)(f1 >> 32);
-                    unsigned a[2] = {h0, h1};
-                    wave_bitonic<2>(a, lane);
-                    auto full_at = [&](int r) -> double {
-                        const unsigned kh = sorted_at<2>(a, r);  // never the pad's ~0u: r < nv
-                        const unsigned long long c0 = __ballot(h0 == kh), c1 = __ballot(h1 == kh);
-                        if (__popcll(c0) + __popcll(c1) == 1)
-                            return dkey_value(c0 ? lane_read(f0, __ffsll((long long)c0) - 1)
-                                                 : lane_read(f1, __ffsll((long long)c1) - 1));
-                        const int rr = r - (__popcll(__ballot(h0 < kh)) + __popcll(__ballot(h1 < kh)));
-                        unsigned long long res = 0;
-                        for (int hh = 0; hh < 2; hh++) {
-                            unsigned long long cm = hh ? c1 : c0;
-                            while (cm) {
-                                const int l = __ffsll((long long)cm) - 1;
-                                cm &= cm - 1;
-                                const unsigned long long e = lane_read(hh ? f1 : f0, l);
-                                const int lt = __popcll(__ballot(h0 == kh && f0 < e)) + __popcll(__ballot(h1 == kh && f1 < e));
-                                const int eq = __popcll(__ballot(f0 == e)) + __popcll(__ballot(f1 == e));
-                                if (rr >= lt && rr < lt + eq) res = e;
+        for (int rep_ = 0; rep_ < REPS(8); rep_++) {  // diagnostic doubling (REPS)
+            // p90 order statistics (:198) by parallel ranks
+            {
+                const double vi = (double)(nv - 1) * 0.9;
+                int r0, r1;
+                if (vi >= (double)(nv - 1)) {
+                    r0 = r1 = nv - 1;
+                } else {
+                    r0 = (int)floor(vi);
+                    r1 = r0 + 1;
+                }
+                if (SKIP(2)) {
+                    if (tid == 0) sh->pa = sh->pb = c.vE[r0];
+                } else if ((FAST || nv <= 128) && !DSP_P90PAR) {
+                    // wave 0: bitonic sort of the high halves of the order-preserving keys; the rank's
+                    // element is the one holding that high half, or, when several do, the one of the
+                    // right rank among them by the full key
+                    if (wid == 0) {
+                        const unsigned long long f0 = lane < nv ? dkey(c.vE[lane]) : ~0ull;
+                        const unsigned long long f1 = lane + 64 < nv ? dkey(c.vE[lane + 64]) : ~0ull;
+                        const unsigned h0 = (unsigned)(f0 >> 32), h1 = (unsigned)(f1 >> 32);
+                        unsigned a[2] = {h0, h1};
+                        wave_bitonic<2>(a, lane);
+                        auto full_at = [&](int r) -> double {
+                            const unsigned kh = sorted_at<2>(a, r);  // never the pad's ~0u: r < nv
+                            const unsigned long long c0 = __ballot(h0 == kh), c1 = __ballot(h1 == kh);
+                            if (__popcll(c0) + __popcll(c1) == 1)
+                                return dkey_value(c0 ? lane_read(f0, __ffsll((long long)c0) - 1)
+                                                     : lane_read(f1, __ffsll((long long)c1) - 1));
+                            const int rr = r - (__popcll(__ballot(h0 < kh)) + __popcll(__ballot(h1 < kh)));
+                            unsigned long long res = 0;
+                            for (int hh = 0; hh < 2; hh++) {
+                                unsigned long long cm = hh ? c1 : c0;
+                                while (cm) {
+                                    const int l = __ffsll((long long)cm) - 1;
+                                    cm &= cm - 1;
+                                    const unsigned long long e = lane_read(hh ? f1 : f0, l);
+                                    const int lt = __popcll(__ballot(h0 == kh && f0 < e)) + __popcll(__ballot(h1 == kh && f1 < e));
+                                    const int eq = __popcll(__ballot(f0 == e)) + __popcll(__ballot(f1 == e));
+                                    if (rr >= lt && rr < lt + eq) res = e;
+                                }
                             }
+                            return dkey_value(res);
+                        };
+                        const double pa = full_at(r0), pb = full_at(r1);
+                        if (lane == 0) {
+                            sh->pa = pa;
+                            sh->pb = pb;
                         }
-                        return dkey_value(res);
-                    };
-                    const double pa = full_at(r0), pb = full_at(r1);
-                    if (lane == 0) {
-                        sh->pa = pa;
-                        sh->pb = pb;
                     }
-                }
-            } else if (nv <= 128) {
-                // order-preserving keys in registers (lane + 64h); wave w takes candidates w,
-                // w + 8, ...: #{keys below} and #{equal keys} by two ballots per half give the
-                // ranks the candidate's value occupies (ties are equal values: no index needed)
-                const unsigned long long k0 = lane < nv ? dkey(c.vE[lane]) : ~0ull;
-                const unsigned long long k1 = lane + 64 < nv ? dkey(c.vE[lane + 64]) : ~0ull;
-                for (int i2 = wid; i2 < nv; i2 += NWAVE) {
-                    const unsigned long long e = lane_read(i2 < 64 ? k0 : k1, i2 & 63);
-                    const int lt = __popcll(__ballot(k0 < e)) + __popcll(__ballot(k1 < e));
-                    const int eq = __popcll(__ballot(k0 == e)) + __popcll(__ballot(k1 == e));
-                    if (lane == 0) {
-                        if (r0 >= lt && r0 < lt + eq) sh->pa = dkey_value(e);
-                        if (r1 >= lt && r1 < lt + eq) sh->pb = dkey_value(e);
+                } else if (nv <= 128) {
+                    // order-preserving keys in registers (lane + 64h); wave w takes candidates w,
+                    // w + 8, ...: #{keys below} and #{equal keys} by two ballots per half give the
+                    // ranks the candidate's value occupies (ties are equal values: no index needed)
+                    const unsigned long long k0 = lane < nv ? dkey(c.vE[lane]) : ~0ull;
+                    const unsigned long long k1 = lane + 64 < nv ? dkey(c.vE[lane + 64]) : ~0ull;
+                    for (int i2 = wid; i2 < nv; i2 += NWAVE) {
+                        const unsigned long long e = lane_read(i2 < 64 ? k0 : k1, i2 & 63);
+                        const int lt = __popcll(__ballot(k0 < e)) + __popcll(__ballot(k1 < e));
+                        const int eq = __popcll(__ballot(k0 == e)) + __popcll(__ballot(k1 == e));
+                        if (lane == 0) {
+                            if (r0 >= lt && r0 < lt + eq) sh->pa = dkey_value(e);
+                            if (r1 >= lt && r1 < lt + eq) sh->pb = dkey_value(e);
+                        }
                     }
-                }
-            } else if (nv <= 256) {
-                ballot_select<double>([&](int j) { return c.vE[j]; }, nv, r0, r1, &sh->pa, &sh->pb, wid, lane);
-            } else {  // long clips: partial ranks over all waves
-                rank_partial([&](int, int j) { return c.vE[j]; }, 1, nv, c.rank, wid, lane);
-                __syncthreads();
-                for (int f = tid; f < nv; f += NT) {
-                    const int r = c.rank[f];
-                    if (r == r0) sh->pa = c.vE[f];
-                    if (r == r1) sh->pb = c.vE[f];
+                } else if (nv <= 256) {
+                    ballot_select<double>([&](int j) { return c.vE[j]; }, nv, r0, r1, &sh->pa, &sh->pb, wid, lane);
+                } else {  // long clips: partial ranks over all waves
+                    rank_partial([&](int, int j) { return c.vE[j]; }, 1, nv, c.rank, wid, lane);
+                    __syncthreads();
+                    for (int f = tid; f < nv; f += NT) {
+                        const int r = c.rank[f];
+                        if (r == r0) sh->pa = c.vE[f];
+                        if (r == r1) sh->pb = c.vE[f];
+                    }
                 }
             }
+            __syncthreads();
         }
-        __syncthreads();
         STAMP(i, 3);
-        if (SKIP(4)) {
-            if (tid == 0) {
-                sh->n3 = 0;
-                sh->n1 = min(30, nv - 1);
-                sh->n6 = min(55, nv - 1);
-                sh->exact = 0;
+        for (int rep_ = 0; rep_ < REPS(16); rep_++) {  // diagnostic doubling (REPS)
+            if (SKIP(4)) {
+                if (tid == 0) {
+                    sh->n3 = 0;
+                    sh->n1 = min(30, nv - 1);
+                    sh->n6 = min(55, nv - 1);
+                    sh->exact = 0;
+                }
+            } else if (wid == 0) {
+                const int flag = vad_scan<!EXACT, FAST>(p, c, nv, lane);
+                if (lane == 0) sh->exact = (!EXACT && Mp > 0.0) ? flag : 0;
             }
-        } else if (wid == 0) {
-            const int flag = vad_scan<!EXACT, FAST>(p, c, nv, lane);
-            if (lane == 0) sh->exact = (!EXACT && Mp > 0.0) ? flag : 0;
+            __syncthreads();
         }
-        __syncthreads();
         if (!EXACT && sh->exact) {  // near tie: redo in numpy's exact order after the loop
             return false;
         }
@@ -1178,8 +1235,8 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
             }
             const float2v y = w * x;
             ea = y * y + ea;
-            ma += fabsf(y.x);
-            mb += fabsf(y.y);
+            ma = add_abs(ma, y.x);
+            mb = add_abs(mb, y.y);
         }
     };
     // one 16-lane row per frame (4 frames per wave): lane rl of the row takes the frame's vectors
@@ -1187,51 +1244,53 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     // sums need four DPP steps instead of a wave reduction
     constexpr int R4_KV = 9;  // vectors per lane in one batch (frames up to 16*9*8-7 samples)
     const int rl = lane & 15, row = lane >> 4;
-    for (int gi = wid; 4 * gi < (SKIP(8) ? 0 : F); gi += NWAVE) {
-        const int g = 4 * gi + row;
-        const bool act = g < F;
-        const int gc = act ? g : F - 1;
-        const int fs = st + gc * S;
-        const int lim = min(L, en - fs);  // samples beyond the crop are zero padding
-        const bool padded = lim < L;
-        const int u0 = lead + fs;
-        const int va = u0 >> 3, vb = (u0 + lim - 1) >> 3;
-        const int r = u0 & 3;  // copy whose rows start at window index = -u0 (mod 4)
-        const float *wr = c.wtab + r * wrow + EXTRACT_WPAD + r;  // wr[j] = w[j], j = -7 .. L + 7
-        float2v ea = {0.f, 0.f};
-        float ma = 0.f, mb = 0.f;
-        for (int v0 = va; v0 <= vb; v0 += 16 * R4_KV) {
-            short8 xv[R4_KV];
+    for (int rep_ = 0; rep_ < REPS(32); rep_++) {  // diagnostic doubling (REPS)
+        for (int gi = wid; 4 * gi < (SKIP(8) ? 0 : F); gi += NWAVE) {
+            const int g = 4 * gi + row;
+            const bool act = g < F;
+            const int gc = act ? g : F - 1;
+            const int fs = st + gc * S;
+            const int lim = min(L, en - fs);  // samples beyond the crop are zero padding
+            const bool padded = lim < L;
+            const int u0 = lead + fs;
+            const int va = u0 >> 3, vb = (u0 + lim - 1) >> 3;
+            const int r = u0 & 3;  // copy whose rows start at window index = -u0 (mod 4)
+            const float *wr = c.wtab + r * wrow + EXTRACT_WPAD + r;  // wr[j] = w[j], j = -7 .. L + 7
+            float2v ea = {0.f, 0.f};
+            float ma = 0.f, mb = 0.f;
+            for (int v0 = va; v0 <= vb; v0 += 16 * R4_KV) {
+                short8 xv[R4_KV];
 #pragma unroll
-            for (int k = 0; k < R4_KV; k++) xv[k] = load_vec(p, cur, min(v0 + rl + 16 * k, vmax));
-            auto run = [&](auto pt, auto nt) {
+                for (int k = 0; k < R4_KV; k++) xv[k] = load_vec(p, cur, min(v0 + rl + 16 * k, vmax));
+                auto run = [&](auto pt, auto nt) {
 #pragma unroll
-                for (int k = 0; k < R4_KV; k++) {
-                    const int v = v0 + rl + 16 * k;
-                    if (v <= vb) frame_vec(pt, nt, xv[k], wr, 8 * v - u0, lim, ea, ma, mb);
-                }
-            };
-            if (padded)
-                run(BoolT<true>(), BoolT<false>());
-            else if (DSP_NEAR0 && near0)
-                run(BoolT<false>(), BoolT<true>());
-            else
-                run(BoolT<false>(), BoolT<false>());
-        }
-        const float E1 = dpp_row_reduce(ea.x + ea.y, OpAdd()) * sE;
-        const float M1 = dpp_row_reduce(ma + mb, OpAdd()) * sM;
-        // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in
-        // [j0, j1]) and j < lim; transitions into the window's zero ends / padding count too
-        const int ia = fs + j0, ib = min(fs + j1, en - 1);  // sample coords
-        int z = dpp_row_reduce(ia < ib ? chg_count(c.posw, ia + lead, ib + lead, rl, 16) : 0, OpAdd());
-        if (ia <= ib) {
-            if (j0 > 0) z += pos_bit(c.posw, ia + lead);
-            if (ib < fs + L - 1) z += pos_bit(c.posw, ib + lead);
-        }
-        if (act && rl == 0) {
-            c.fE[g] = E1;
-            c.fM[g] = M1;
-            c.fZ[g] = z;
+                    for (int k = 0; k < R4_KV; k++) {
+                        const int v = v0 + rl + 16 * k;
+                        if (v <= vb) frame_vec(pt, nt, xv[k], wr, 8 * v - u0, lim, ea, ma, mb);
+                    }
+                };
+                if (padded)
+                    run(BoolT<true>(), BoolT<false>());
+                else if (DSP_NEAR0 && near0)
+                    run(BoolT<false>(), BoolT<true>());
+                else
+                    run(BoolT<false>(), BoolT<false>());
+            }
+            const float E1 = dpp_row_reduce(ea.x + ea.y, OpAdd()) * sE;
+            const float M1 = dpp_row_reduce(ma + mb, OpAdd()) * sM;
+            // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in
+            // [j0, j1]) and j < lim; transitions into the window's zero ends / padding count too
+            const int ia = fs + j0, ib = min(fs + j1, en - 1);  // sample coords
+            int z = dpp_row_reduce(ia < ib ? chg_count(c.posw, ia + lead, ib + lead, rl, 16) : 0, OpAdd());
+            if (ia <= ib) {
+                if (j0 > 0) z += pos_bit(c.posw, ia + lead);
+                if (ib < fs + L - 1) z += pos_bit(c.posw, ib + lead);
+            }
+            if (act && rl == 0) {
+                c.fE[g] = E1;
+                c.fM[g] = M1;
+                c.fZ[g] = z;
+            }
         }
     }
     if (!FAST && F > 128)
@@ -1242,89 +1301,91 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     // ---- R5: 15-d statistics (compute_statistics x 3, fe.py:46-62) ------------------------
     // np.median: the middle order statistic (odd F) or the mean of the two middle ones
     const int r0 = (F - 1) / 2, r1 = F / 2;
-    if (FAST || F <= 128) {
-        // wave q alone handles sequence q (E, M, ZCR): lanes hold v[lane], v[lane + 64]; the
-        // order statistics by ballot ranks over readlane'd candidates, then mean / std (fp64 sums)
-        // and max / min -- no barrier
-        if (wid < (DSP_R5SPLIT ? 6 : 3) && !SKIP(48)) {
-            const int q = wid % 3;
-            auto get = [&](int j) -> float { return q == 0 ? c.fE[j] : q == 1 ? c.fM[j] : (float)c.fZ[j]; };
-            const bool in0 = lane < F, in1 = lane + 64 < F;
-            const float x0 = in0 ? get(lane) : 0.f, x1 = in1 ? get(lane + 64) : 0.f;
-            if (wid < 3 || !DSP_R5SPLIT) {  // median by an in-wave bitonic sort
-                unsigned a[2] = {in0 ? fkey(x0) : ~0u, in1 ? fkey(x1) : ~0u};
-                float v0, v1;
-                if (F <= 64) {
-                    unsigned b[1] = {a[0]};
-                    wave_bitonic<1>(b, lane);
-                    v0 = fkey_value(sorted_at<1>(b, r0));
-                    v1 = fkey_value(sorted_at<1>(b, r1));
-                } else {
-                    wave_bitonic<2>(a, lane);
-                    v0 = fkey_value(sorted_at<2>(a, r0));
-                    v1 = fkey_value(sorted_at<2>(a, r1));
+    for (int rep_ = 0; rep_ < REPS(64); rep_++) {  // diagnostic doubling (REPS)
+        if (FAST || F <= 128) {
+            // wave q alone handles sequence q (E, M, ZCR): lanes hold v[lane], v[lane + 64]; the
+            // order statistics by ballot ranks over readlane'd candidates, then mean / std (fp64 sums)
+            // and max / min -- no barrier
+            if (wid < (DSP_R5SPLIT ? 6 : 3) && !SKIP(48)) {
+                const int q = wid % 3;
+                auto get = [&](int j) -> float { return q == 0 ? c.fE[j] : q == 1 ? c.fM[j] : (float)c.fZ[j]; };
+                const bool in0 = lane < F, in1 = lane + 64 < F;
+                const float x0 = in0 ? get(lane) : 0.f, x1 = in1 ? get(lane + 64) : 0.f;
+                if (wid < 3 || !DSP_R5SPLIT) {  // median by an in-wave bitonic sort
+                    unsigned a[2] = {in0 ? fkey(x0) : ~0u, in1 ? fkey(x1) : ~0u};
+                    float v0, v1;
+                    if (F <= 64) {
+                        unsigned b[1] = {a[0]};
+                        wave_bitonic<1>(b, lane);
+                        v0 = fkey_value(sorted_at<1>(b, r0));
+                        v1 = fkey_value(sorted_at<1>(b, r1));
+                    } else {
+                        wave_bitonic<2>(a, lane);
+                        v0 = fkey_value(sorted_at<2>(a, r0));
+                        v1 = fkey_value(sorted_at<2>(a, r1));
+                    }
+                    double med;
+                    {
+#pragma clang fp contract(off)
+                        med = (F & 1) ? (double)v1 : ((double)v0 + (double)v1) / 2.0;
+                    }
+                    if (lane == 0) featb[5 * q + 4] = (float)med;
                 }
+                if (wid >= 3 || !DSP_R5SPLIT) {  // mean, population std (fp64 sums), max, min
+                    const double s = wave_sum((in0 ? (double)x0 : 0.0) + (in1 ? (double)x1 : 0.0));
+                    const float mx = wave_reduce(fmaxf(in0 ? x0 : -INFINITY, in1 ? x1 : -INFINITY), OpMax());
+                    const float mn = wave_reduce(fminf(in0 ? x0 : INFINITY, in1 ? x1 : INFINITY), OpMin());
+                    const double mean = s / (double)F;
+                    const double d0 = in0 ? (double)x0 - mean : 0.0, d1 = in1 ? (double)x1 - mean : 0.0;
+                    const double qq = wave_sum(fma(d0, d0, d1 * d1));
+                    if (lane < 4) {
+                        const double o = lane == 0 ? mean : lane == 1 ? sqrt(qq / (double)F) : lane == 2 ? (double)mx
+                                         : (double)mn;
+                        featb[5 * q + lane] = (float)o;
+                    }
+                }
+            }
+        } else {  // long sequences: partial ranks over all waves, then one wave per sequence
+            rank_partial([&](int q, int j) { return q == 2 ? (float)c.fZ[j] : (q == 0 ? c.fE[j] : c.fM[j]); },
+                         3, F, c.rank, wid, lane);
+            __syncthreads();
+            for (int t = tid; t < 3 * F; t += NT) {
+                const int q = t / F, e = t - q * F;
+                const int r = c.rank[t];
+                const double val = q == 2 ? (double)c.fZ[e] : (double)(q == 0 ? c.fE[e] : c.fM[e]);
+                if (r == r0) sh->oslo[q] = val;
+                if (r == r1) sh->oshi[q] = val;
+            }
+            __syncthreads();
+            if (wid < 3) {
+                double s = 0.0, mx = -INFINITY, mn = INFINITY;
+                for (int q = lane; q < F; q += 64) {
+                    const double x = wid == 0 ? (double)c.fE[q] : wid == 1 ? (double)c.fM[q] : (double)c.fZ[q];
+                    s += x;
+                    mx = fmax(mx, x);
+                    mn = fmin(mn, x);
+                }
+                s = wave_sum(s);
+                mx = wave_maxd(mx);
+                mn = wave_mind(mn);
+                const double mean = s / (double)F;
+                double qq = 0.0;
+                for (int q = lane; q < F; q += 64) {
+                    const double x = wid == 0 ? (double)c.fE[q] : wid == 1 ? (double)c.fM[q] : (double)c.fZ[q];
+                    const double d = x - mean;
+                    qq = fma(d, d, qq);
+                }
+                qq = wave_sum(qq);
                 double med;
                 {
 #pragma clang fp contract(off)
-                    med = (F & 1) ? (double)v1 : ((double)v0 + (double)v1) / 2.0;
+                    med = (F & 1) ? sh->oshi[wid] : (sh->oslo[wid] + sh->oshi[wid]) / 2.0;
                 }
-                if (lane == 0) featb[5 * q + 4] = (float)med;
-            }
-            if (wid >= 3 || !DSP_R5SPLIT) {  // mean, population std (fp64 sums), max, min
-                const double s = wave_sum((in0 ? (double)x0 : 0.0) + (in1 ? (double)x1 : 0.0));
-                const float mx = wave_reduce(fmaxf(in0 ? x0 : -INFINITY, in1 ? x1 : -INFINITY), OpMax());
-                const float mn = wave_reduce(fminf(in0 ? x0 : INFINITY, in1 ? x1 : INFINITY), OpMin());
-                const double mean = s / (double)F;
-                const double d0 = in0 ? (double)x0 - mean : 0.0, d1 = in1 ? (double)x1 - mean : 0.0;
-                const double qq = wave_sum(fma(d0, d0, d1 * d1));
-                if (lane < 4) {
-                    const double o = lane == 0 ? mean : lane == 1 ? sqrt(qq / (double)F) : lane == 2 ? (double)mx
-                                     : (double)mn;
-                    featb[5 * q + lane] = (float)o;
+                if (lane < 5) {
+                    const double o = lane == 0 ? mean : lane == 1 ? sqrt(qq / (double)F) : lane == 2 ? mx
+                                     : lane == 3 ? mn : med;
+                    featb[5 * wid + lane] = (float)o;
                 }
-            }
-        }
-    } else {  // long sequences: partial ranks over all waves, then one wave per sequence
-        rank_partial([&](int q, int j) { return q == 2 ? (float)c.fZ[j] : (q == 0 ? c.fE[j] : c.fM[j]); },
-                     3, F, c.rank, wid, lane);
-        __syncthreads();
-        for (int t = tid; t < 3 * F; t += NT) {
-            const int q = t / F, e = t - q * F;
-            const int r = c.rank[t];
-            const double val = q == 2 ? (double)c.fZ[e] : (double)(q == 0 ? c.fE[e] : c.fM[e]);
-            if (r == r0) sh->oslo[q] = val;
-            if (r == r1) sh->oshi[q] = val;
-        }
-        __syncthreads();
-        if (wid < 3) {
-            double s = 0.0, mx = -INFINITY, mn = INFINITY;
-            for (int q = lane; q < F; q += 64) {
-                const double x = wid == 0 ? (double)c.fE[q] : wid == 1 ? (double)c.fM[q] : (double)c.fZ[q];
-                s += x;
-                mx = fmax(mx, x);
-                mn = fmin(mn, x);
-            }
-            s = wave_sum(s);
-            mx = wave_maxd(mx);
-            mn = wave_mind(mn);
-            const double mean = s / (double)F;
-            double qq = 0.0;
-            for (int q = lane; q < F; q += 64) {
-                const double x = wid == 0 ? (double)c.fE[q] : wid == 1 ? (double)c.fM[q] : (double)c.fZ[q];
-                const double d = x - mean;
-                qq = fma(d, d, qq);
-            }
-            qq = wave_sum(qq);
-            double med;
-            {
-#pragma clang fp contract(off)
-                med = (F & 1) ? sh->oshi[wid] : (sh->oslo[wid] + sh->oshi[wid]) / 2.0;
-            }
-            if (lane < 5) {
-                const double o = lane == 0 ? mean : lane == 1 ? sqrt(qq / (double)F) : lane == 2 ? mx
-                                 : lane == 3 ? mn : med;
-                featb[5 * wid + lane] = (float)o;
             }
         }
     }
