@@ -216,24 +216,18 @@ __device__ __forceinline__ void two_prod(double a, double b, double &p, double &
     e = __fma_rn(a, b, -p);
 }
 
-// sum_{frame} (k - mq)^2 / M'^2 from the exact moments S1 = sum k, S2 = sum k^2 (L samples):
-// S2 - 2 mq S1 + L mq^2 evaluated in double-double (cancellation-free), then one division.
-__device__ double energy_from_moments(unsigned long long S2, long long S1, int L, double mq, double Mp)
+// sum_{frame} (k - mq)^2 / M'^2 from the exact moments S1 = sum k, S2 = sum k^2 (L samples).
+// With d = k - t0 (t0 = round(mq), delta = mq - t0 exact, |delta| <= 1/2) the moments of d are
+// exact integers D1, D2 (< 2^53), and sum (d - delta)^2 = D2 - 2 delta D1 + L delta^2 >= D2 / 4
+// (every |d - delta| >= |d| / 2 for d != 0): no cancellation, so plain double evaluation is within
+// a few ulp -- far inside the 1e-11 certification margin of the endpoint decisions.
+__device__ __forceinline__ double energy_from_moments(unsigned long long S2, long long S1, int L, int t0,
+                                                      double delta, double invM2)
 {
-    if (!(Mp > 0.0)) return 0.0;  // constant clip: preprocess leaves zeros (:73-75)
-    const double s2 = (double)S2, s1 = (double)S1;
-    double p, pe, q, qe, r, re;
-    two_prod(mq, s1, p, pe);
-    p *= 2.0;
-    pe *= 2.0;
-    two_prod(mq, mq, q, qe);
-    two_prod((double)L, q, r, re);
-    re += (double)L * qe;
-    double a, ae, b, be;
-    two_sum(s2, -p, a, ae);
-    two_sum(a, r, b, be);
-    const double A = b + (((ae + be) - pe) + re);
-    return A / (Mp * Mp);
+    const long long D1 = S1 - (long long)L * t0;
+    const long long D2 = (long long)S2 - 2LL * t0 * S1 + (long long)L * t0 * t0;
+    const double r = fma(-2.0 * delta, (double)D1, (double)D2) + (double)L * delta * delta;
+    return r * invM2;  // invM2 = 0 for a constant clip: preprocess leaves zeros (:73-75)
 }
 
 // numpy float64 summation order (pairwise_sum in 8192-element buffered chunks): the certified
@@ -944,6 +938,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     const int t0 = (int)floor(mq + 0.5);
     const float deltaf = (float)(mq - (double)t0);  // mq - t0 is exact (Sterbenz)
     const float invMf = Mp > 0.0 ? __builtin_amdgcn_rcpf((float)Mp) : 0.0f;  // scale only: 1 ulp
+    const double invM2 = Mp > 0.0 ? 1.0 / (Mp * Mp) : 0.0;  // endpoint energies (one rounding)
     const int nv = (p.do_vad && n >= L) ? (n - L) / S + 1 : 0;
     STAMP(i, 1);
 
@@ -1079,7 +1074,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                 if (act && lq == 0) {
                     c.rank[f] = 0;
                     c.vE[f] = EXACT ? np_energy_exact(clip_g, f * S, L, mq, Mp)
-                                    : energy_from_moments(s2, s1, L, mq, Mp);
+                                    : energy_from_moments(s2, s1, L, t0, mq - (double)t0, invM2);
                     c.vZ[f] = zc;
                 }
             }
