@@ -40,8 +40,8 @@
 #ifndef DSP_R5SPLIT
 #define DSP_R5SPLIT 1  // R5: medians and moments on separate waves
 #endif
-#ifndef DSP_IW1
-#define DSP_IW1 0  // word loads from one address when inside the clip (measured slower)
+#ifndef DSP_BUFLOAD
+#define DSP_BUFLOAD 1  // clip loads through a range-checked buffer descriptor
 #endif
 #ifndef DSP_ASM_ABS
 #define DSP_ASM_ABS 1  // R4: M += |y| as one VOP3 add with the abs modifier
@@ -386,27 +386,41 @@ struct Ctx {
     int stamp_clip;  // clip index for the diagnostic stamps
 };
 
-// 16-B vectors of the clip buffer.  The buffer's last vector may reach up to 15 bytes past
-// offsets[B]; pcm is 16-B aligned, so such a vector never crosses a page and the read cannot
-// fault.  Bytes outside a clip are masked by every consumer ([lead, lead + n) ranges, zero window
-// weights), so no element-wise patching is needed.
+// 16-B vectors of the clip buffer, read through a buffer descriptor spanning the clip's vectors
+// (DSP_BUFLOAD): a vector index past the clip reads zeros (hardware range check), so no address
+// clamping, and the four vectors of a word share one offset register (immediate offsets).  The
+// clip's last vector may reach up to 15 bytes past offsets[B]; pcm is 16-B aligned, so such a
+// vector never crosses a page.  Bytes outside a clip are masked by every consumer ([lead, lead + n)
+// ranges, zero window weights), so no element-wise patching is needed.
+#if DSP_BUFLOAD
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t clip_rsrc(const ExtractParams &p, const ClipRef &c)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<int16_t *>(p.pcm + c.base), 0, c.nvec * 16, 0x00020000);
+}
 __device__ __forceinline__ short8 load_vec(const ExtractParams &p, const ClipRef &c, int v)
 {
-    return reinterpret_cast<const short8 *>(p.pcm + c.base)[v];
+    return __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(clip_rsrc(p, c), 16 * v, 0, 0));
+}
+__device__ __forceinline__ void issue_word(short8 *q, const ExtractParams &p, const ClipRef &c, int w)
+{
+    const __amdgpu_buffer_rsrc_t rs = clip_rsrc(p, c);
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        q[k] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rs, 64 * w + 16 * k, 0, 0));
+}
+#else
+__device__ __forceinline__ short8 load_vec(const ExtractParams &p, const ClipRef &c, int v)
+{
+    return reinterpret_cast<const short8 *>(p.pcm + c.base)[min(v, c.nvec - 1)];
 }
 // the four 16-B loads of word w (unconditional, clamped to the clip's last vector)
 __device__ __forceinline__ void issue_word(short8 *q, const ExtractParams &p, const ClipRef &c, int w)
 {
     const short8 *src = reinterpret_cast<const short8 *>(p.pcm + c.base);
-    if (DSP_IW1 && 4 * w + 3 < c.nvec) {  // one address, immediate offsets
-        const short8 *a = src + 4 * w;
 #pragma unroll
-        for (int k = 0; k < 4; k++) q[k] = a[k];
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; k++) q[k] = src[min(4 * w + k, c.nvec - 1)];
-    }
+    for (int k = 0; k < 4; k++) q[k] = src[min(4 * w + k, c.nvec - 1)];
 }
+#endif
 
 // acc + |v| in one VOP3 add with the abs source modifier
 __device__ __forceinline__ float add_abs(float acc, float v)
@@ -1018,7 +1032,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                     if (pw >= 0) {
                         short8 q[4];
 #pragma unroll
-                        for (int k = 0; k < 4; k++) q[k] = load_vec(p, cur, min(4 * pw + k, cur.nvec - 1));
+                        for (int k = 0; k < 4; k++) q[k] = load_vec(p, cur, 4 * pw + k);
 #pragma unroll 1
                         for (int k = 0; k < 4; k++) {
                             const short8 v = k == 0 ? q[0] : k == 1 ? q[1] : k == 2 ? q[2] : q[3];
@@ -1201,7 +1215,6 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     // Per sample y = w_j * x (the reference's windowed frame, :329-331), E += y^2, M += |y|:
     // the weights of a vector's 8 samples are two aligned 16-B reads from the window copy
     // shifted by u0 mod 4; x pairs go through packed fp32 ops.
-    const int vmax = cur.nvec - 1;
     const int wrow = EXTRACT_WROW(L);
     typedef float float2v __attribute__((ext_vector_type(2)));
     const float2v mt = {-t0f, -t0f}, md = {-deltaf, -deltaf};
@@ -1256,7 +1269,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
             for (int v0 = va; v0 <= vb; v0 += 16 * R4_KV) {
                 short8 xv[R4_KV];
 #pragma unroll
-                for (int k = 0; k < R4_KV; k++) xv[k] = load_vec(p, cur, min(v0 + rl + 16 * k, vmax));
+                for (int k = 0; k < R4_KV; k++) xv[k] = load_vec(p, cur, v0 + rl + 16 * k);
                 auto run = [&](auto pt, auto nt) {
 #pragma unroll
                     for (int k = 0; k < R4_KV; k++) {

@@ -7,7 +7,7 @@ import torch
 from src.pipeline import FeatureExtractor
 from src.synth import make_batch
 
-def timeit(fx, x, reps=20):
+def timeit(fx, x, reps=50):
     for _ in range(3): fx(x)
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
