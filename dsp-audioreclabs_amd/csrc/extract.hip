@@ -344,6 +344,7 @@ struct Shared {
     long long red_k[NWAVE];
     int red_a[NWAVE], red_b[NWAVE];
     double pa, pb;            // the two order statistics of the VAD energies around p90
+    double noise_e, noise_z;  // VAD noise estimates (:189-195, :239-245)
     double oslo[3], oshi[3];  // order statistics (F-1)/2 and F/2 of E, M, ZCR (medians)
     int n3, n1, n6, exact, j0, j1, ndefer;
 };
@@ -537,15 +538,12 @@ __device__ __forceinline__ bool bits_any_in(const BitsK<KC> &m, int lo, int hi) 
     return f >= 0 && f < hi;
 }
 
-// Double-threshold endpoint scan (src/audio_processing.py:186-273) by wave 0 on vE/vZ with the
-// p90 order statistics in sh->pa / sh->pb.  Writes sh->n3 (-1: no high-energy frame), n1, n6;
-// returns the near-tie flag.
-template <bool CERTIFY, bool FAST>
-__device__ __forceinline__ int vad_scan(const ExtractParams &p, const Ctx &c, int nv, int lane)
+// VAD noise estimates (src/audio_processing.py:188-195, :239-245) by one wave into sh->noise_e /
+// sh->noise_z, computed while wave 0 selects the p90 order statistics
+__device__ __forceinline__ void vad_noise(const Ctx &c, int nv, int lane)
 {
     const double *vE = c.vE;
     const int32_t *vZ = c.vZ;
-    Shared *sh = c.sh;
     const int nfr = min(5, nv / 10);  // :188
     double noise_e, noise_z;
     if (nfr > 0) {  // :189-193, :239-243 (every lane computes the same numpy-order sum)
@@ -565,6 +563,22 @@ __device__ __forceinline__ int vad_scan(const ExtractParams &p, const Ctx &c, in
         noise_e = wave_mind(me);
         noise_z = (double)wave_min(mz);
     }
+    if (lane == 0) {
+        c.sh->noise_e = noise_e;
+        c.sh->noise_z = noise_z;
+    }
+}
+
+// Double-threshold endpoint scan (src/audio_processing.py:186-273) by wave 0 on vE/vZ with the
+// p90 order statistics in sh->pa / sh->pb.  Writes sh->n3 (-1: no high-energy frame), n1, n6;
+// returns the near-tie flag.
+template <bool CERTIFY, bool FAST>
+__device__ __forceinline__ int vad_scan(const ExtractParams &p, const Ctx &c, int nv, int lane)
+{
+    const double *vE = c.vE;
+    const int32_t *vZ = c.vZ;
+    Shared *sh = c.sh;
+    const double noise_e = sh->noise_e, noise_z = sh->noise_z;  // vad_noise, another wave
     // np.percentile(E, 90) (:198): lerp of the two order statistics found by the workgroup
     const double vi = (double)(nv - 1) * 0.9;
     const double g = (vi >= (double)(nv - 1)) ? vi + 1.0 : vi - floor(vi);
@@ -1172,6 +1186,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                     }
                 }
             }
+            if (wid == 1 % NWAVE) vad_noise(c, nv, lane);  // beside wave 0's p90 selection
             __syncthreads();
         }
         STAMP(i, 3);
