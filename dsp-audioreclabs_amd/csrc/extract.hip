@@ -1482,9 +1482,13 @@ __device__ __forceinline__ Ctx make_ctx(const ExtractParams &p, unsigned char *l
 
 // the rare near-tie redo, compiled out of line so its exact-order machinery does not weigh on
 // the register allocation of the streaming path
+// The kernel arguments are read in place from the kernel-argument segment: passing them by value
+// would copy the struct to scratch at every kernel entry (all lanes of every wave, ~24 MB of HBM
+// writes per 1000-clip launch).
 template <bool FAST>
-__device__ __attribute__((noinline)) void clip_exact(const ExtractParams p, int i)
+__device__ __attribute__((noinline)) void clip_exact(int i)
 {
+    const ExtractParams &p = *(const ExtractParams *)__builtin_amdgcn_kernarg_segment_ptr();
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     Ctx c = make_ctx<FAST>(p, lds);
     c.stamp_clip = i;
@@ -1576,7 +1580,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     const int nd = sh->ndefer;
     for (int d = 0; d < nd; d++) {
         const int j = c.defer[d];
-        clip_exact<FAST>(p, j);
+        clip_exact<FAST>(j);
         __syncthreads();
     }
     WG_STAMP(22);
