@@ -29,7 +29,6 @@
 //   * windowed E/M: fp32 on VALU (tolerance 1e-5 rel., measured ~2e-7); statistics in fp64.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 
 #include "dsp_audiorec.h"
 #include "extract_layout.h"
@@ -1499,15 +1498,22 @@ __device__ __attribute__((noinline)) void clip_exact(int i)
     clip_body<true, FAST>(p, c, i, cr, regs);
 }
 
-// window (create_window, :278-296) -> LDS as four shifted zero-padded fp32 copies (c.wtab) and
-// its support [j0, j1] (sh->j0 / j1) by ballots; ends with a barrier
+// 128 VGPRs: two 512-thread workgroups per CU
+#ifndef EXTRACT_WAVES_PER_EU
+#define EXTRACT_WAVES_PER_EU 4
+#endif
 template <bool FAST>
-__device__ __forceinline__ void extract_window_prologue(const ExtractParams &p, const Ctx &c)
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVES_PER_EU))) void extract_kernel(ExtractParams p)
 {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    Ctx c = make_ctx<FAST>(p, lds);
     float *wt = const_cast<float *>(c.wtab);
     Shared *sh = c.sh;
+
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int L = p.L;
+    const int L = p.L, G = gridDim.x;
+    WG_STAMP(16);
+
     // window (create_window, :278-296) -> LDS once as four shifted zero-padded fp32 copies, and
     // its support [j0, j1] by ballots: every weight read is issued before the first use, so the
     // prologue costs one L2 round trip (windows longer than WPRE * NT loop over the rest).
@@ -1522,6 +1528,7 @@ __device__ __forceinline__ void extract_window_prologue(const ExtractParams &p, 
     if (tid == 0) {
         sh->j0 = L;
         sh->j1 = -1;
+        sh->ndefer = 0;
     }
     const int wrow = EXTRACT_WROW(L);
     for (int t = tid; t < 4 * (wrow - L); t += NT) {  // zero pads: m < WPAD + r, m >= L + WPAD + r
@@ -1548,24 +1555,6 @@ __device__ __forceinline__ void extract_window_prologue(const ExtractParams &p, 
     for (int q0 = NT * WPRE + wid * 64; q0 < L; q0 += NT) put_weight(q0, q0 + lane < L ? p.window[q0 + lane] : 0.0);
     __syncthreads();
     WG_CK(20);
-}
-
-// 128 VGPRs: two 512-thread workgroups per CU
-#ifndef EXTRACT_WAVES_PER_EU
-#define EXTRACT_WAVES_PER_EU 4
-#endif
-template <bool FAST>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVES_PER_EU))) void extract_kernel(ExtractParams p)
-{
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    Ctx c = make_ctx<FAST>(p, lds);
-    Shared *sh = c.sh;
-
-    const int tid = threadIdx.x, G = gridDim.x;
-    WG_STAMP(16);
-
-    if (tid == 0) sh->ndefer = 0;  // read after the prologue's barriers
-    extract_window_prologue<FAST>(p, c);
 
     short8 regs[NRV];
     for (int i = blockIdx.x; i < p.B; i += G) {
@@ -1599,8 +1588,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
 
 }  // namespace dsp
 
-#include "extract_hop.h"
-
 static void *g_stamp_buffer = nullptr;
 static int g_skip = 0;
 #ifdef DSP_STAMPS
@@ -1625,11 +1612,6 @@ extern "C" size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int f
 }
 
 static int g_num_cus = 0;
-// DSP_EXTRACT_KERNEL=generic forces extract_kernel everywhere (A/B timing, parity cross-checks)
-static const bool g_use_hop = [] {
-    const char *e = getenv("DSP_EXTRACT_KERNEL");
-    return !(e && e[0] == 'g');
-}();
 
 extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, int B,
                                     int64_t max_len, int frame_length, int frame_shift,
@@ -1658,10 +1640,6 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
         (void)hipFuncSetAttribute((const void *)dsp::extract_kernel<false>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
-        (void)hipFuncSetAttribute((const void *)dsp::hop_kernel<7, 3, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
-        (void)hipFuncSetAttribute((const void *)dsp::hop_kernel<8, 2, false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
     }
     dsp::ExtractParams p;
     p.pcm = pcm;
@@ -1687,36 +1665,6 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     p.stamps = (unsigned long long *)g_stamp_buffer;
     p.cv = extract_carve((int)max_len, frame_length, frame_shift, EXTRACT_DEFER_CAP);
     p.skip = g_skip;
-    // hop-major kernel (extract_hop.h) for the frame geometries it is built for
-    if (g_use_hop) {
-        const int L = frame_length, S = frame_shift;
-        int C = 0;
-        if (S % 7 == 0 && (S / 7 == 63 || S / 7 == 64)) C = 7;
-        else if (S == 512) C = 8;
-        const int D = (L + S - 1) / S;
-        const int r = L - (D - 1) * S;
-        const int fall = max_len <= L ? 1 : (int)((max_len - L + S - 1) / S) + 1;
-        const bool fits = extract_fast_fits((int)max_len, L, S) && fall - 1 + D <= dsp::HMAX && fall <= 128 &&
-                          (max_len >= L ? (max_len - L) / S + 1 : 0) <= 128;
-        const bool k73 = C == 7 && D == 3 && r < S, k82 = C == 8 && D == 2 && r == S;
-        if (fits && (k73 || k82)) {
-            dsp::HopGeo hg;
-            hg.nch = S / C;
-            hg.r = r;
-            hg.ciA = r / C;
-            hg.eA = r - C * hg.ciA;
-            const int slots = HOP_WG_PER_CU * g_num_cus;
-            const int grid = B < slots ? B : slots;
-            if (k73)
-                hipLaunchKernelGGL((dsp::hop_kernel<7, 3, true>), dim3(grid), dim3(dsp::NT), (size_t)dsp::HOP_LDS_TOTAL,
-                                   (hipStream_t)stream, p, hg);
-            else
-                hipLaunchKernelGGL((dsp::hop_kernel<8, 2, false>), dim3(grid), dim3(dsp::NT), (size_t)dsp::HOP_LDS_TOTAL,
-                                   (hipStream_t)stream, p, hg);
-            const hipError_t e = hipGetLastError();
-            return e == hipSuccess ? DSP_OK : DSP_ERR_HIP + (int)e;
-        }
-    }
     // persistent grid: two workgroups per CU when their LDS fits (one otherwise), each walking
     // clips blockIdx, blockIdx + grid, ...; the compile-time layout whenever the launch fits it
     const bool fast = extract_fast_fits((int)max_len, frame_length, frame_shift);
