@@ -19,6 +19,7 @@
 //   5. vote           majority label, smallest label on ties (scipy.stats.mode).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "dsp_audiorec.h"
 
@@ -26,19 +27,29 @@ namespace dsp {
 
 static constexpr int KNN_TQ = 256;   // queries per screening workgroup (one per thread)
 static constexpr int KNN_TR = 256;   // reference rows per LDS tile
-static constexpr int KNN_SLACK = 4;  // extra screened candidates per split
+static constexpr int KNN_SLACK = 3;  // extra screened candidates per split (k = 5 -> 8)
+static constexpr int KNN_RU = 4;     // reference rows per unrolled step of the screen
 
-__global__ void knn_convert(const double *__restrict__ src, int64_t N, int D, int DP,
+// mode 0: plain rows (v, 0 ...); mode 1 (reference, expanded form): (-2 v, 0 ..., |v|^2);
+// mode 2 (query, expanded form): (v, 0 ..., 1) -- so that |q - r|^2 = |q|^2 + q'.r'
+__global__ void knn_convert(const double *__restrict__ src, int64_t N, int D, int DP, int mode,
                             float *__restrict__ dst, unsigned int *maxnorm_bits)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     float nrm = 0.f;
     if (i < N) {
+        double n64 = 0.0;
         for (int c = 0; c < DP; c++) {
-            float v = c < D ? (float)src[i * D + c] : 0.f;
-            dst[i * DP + c] = v;
+            const double x = c < D ? src[i * D + c] : 0.0;
+            const float v = (float)x;
             nrm = fmaf(v, v, nrm);
+            n64 = fma(x, x, n64);
+            float o = v;
+            if (mode == 1) o = c < D ? (float)(-2.0 * x) : 0.f;
+            if (mode == 2 && c == DP - 1) o = 1.f;
+            dst[i * DP + c] = o;
         }
+        if (mode == 1) dst[i * DP + DP - 1] = (float)n64;
     }
     // block max -> one atomic (non-negative floats order like their bit patterns)
     for (int o = 32; o > 0; o >>= 1) nrm = fmaxf(nrm, __shfl_xor(nrm, o, 64));
@@ -68,7 +79,7 @@ __device__ __forceinline__ void topk_insert(float (&dl)[KC], int (&il)[KC], floa
     }
 }
 
-template <int DP, int KC>
+template <int DP, int KC, bool EXP>
 __global__ __launch_bounds__(KNN_TQ) void knn_screen(const float *__restrict__ ref32, int64_t Nr,
                                                       const float *__restrict__ q32, int64_t Nq,
                                                       int64_t self_offset, int nsplit,
@@ -84,6 +95,9 @@ __global__ __launch_bounds__(KNN_TQ) void knn_screen(const float *__restrict__ r
     float qv[DP];
 #pragma unroll
     for (int c = 0; c < DP; c++) qv[c] = q < Nq ? q32[q * DP + c] : 0.f;
+    float qn = 0.f;  // expanded form: |q|^2 + sum q'_c r'_c, one FMA per dimension
+#pragma unroll
+    for (int c = 0; c < DP - 1; c++) qn = fmaf(qv[c], qv[c], qn);
     const int64_t self = (self_offset >= 0 && q < Nq) ? self_offset + q : -1;
     float dl[KC];
     int il[KC];
@@ -103,21 +117,35 @@ __global__ __launch_bounds__(KNN_TQ) void knn_screen(const float *__restrict__ r
             reinterpret_cast<float4 *>(tile)[e] = v;
         }
         __syncthreads();
-        for (int j = 0; j < nt; j++) {
-            const float4 *rv = reinterpret_cast<const float4 *>(tile + j * DP);
-            float d = 0.f;
+        // rows in groups of KNN_RU: independent FMA chains, then the inserts in row order
+        for (int j0 = 0; j0 < nt; j0 += KNN_RU) {
+            float d[KNN_RU];
 #pragma unroll
-            for (int c4 = 0; c4 < DP / 4; c4++) {
-                const float4 r = rv[c4];
-                float t;
-                t = qv[4 * c4 + 0] - r.x; d = fmaf(t, t, d);
-                t = qv[4 * c4 + 1] - r.y; d = fmaf(t, t, d);
-                t = qv[4 * c4 + 2] - r.z; d = fmaf(t, t, d);
-                t = qv[4 * c4 + 3] - r.w; d = fmaf(t, t, d);
+            for (int u = 0; u < KNN_RU; u++) {
+                const float4 *rv = reinterpret_cast<const float4 *>(tile + (j0 + u) * DP);  // rows >= nt are zero
+                d[u] = EXP ? qn : 0.f;
+#pragma unroll
+                for (int c4 = 0; c4 < DP / 4; c4++) {
+                    const float4 r = rv[c4];
+                    if (EXP) {
+                        d[u] = fmaf(qv[4 * c4 + 0], r.x, d[u]);
+                        d[u] = fmaf(qv[4 * c4 + 1], r.y, d[u]);
+                        d[u] = fmaf(qv[4 * c4 + 2], r.z, d[u]);
+                        d[u] = fmaf(qv[4 * c4 + 3], r.w, d[u]);
+                    } else {
+                        float t;
+                        t = qv[4 * c4 + 0] - r.x; d[u] = fmaf(t, t, d[u]);
+                        t = qv[4 * c4 + 1] - r.y; d[u] = fmaf(t, t, d[u]);
+                        t = qv[4 * c4 + 2] - r.z; d[u] = fmaf(t, t, d[u]);
+                        t = qv[4 * c4 + 3] - r.w; d[u] = fmaf(t, t, d[u]);
+                    }
+                }
             }
-            const int64_t r = t0 + j;
-            if (r == self) d = INFINITY;
-            topk_insert<KC>(dl, il, d, (int)r);
+#pragma unroll
+            for (int u = 0; u < KNN_RU; u++) {
+                const int64_t r = t0 + j0 + u;
+                if (j0 + u < nt && r != self) topk_insert<KC>(dl, il, d[u], (int)r);
+            }
         }
     }
     if (q < Nq) {
@@ -209,22 +237,53 @@ __global__ void knn_merge(const double *__restrict__ ref, const double *__restri
     }
     double qn = 0.0;
     for (int c = 0; c < D; c++) qn += qx[c] * qx[c];
-    // screening cut-off of every split whose candidate list is full
+    // |fp32 screened distance - fp64 distance| <= err(d): fp32 rounding of the inputs and of the
+    // sum (direct or expanded form)
+    const double rmax = (double)__uint_as_float(*maxnorm_bits);
+    // (expanded form: 16 FMA roundings of partial sums bounded by 2 (|q|^2 + |r|^2))
+    auto err = [&](double d) { return 2e-6 * d + 4e-6 * (qn + rmax) + 1e-30; };
+    // pass 1 (fp32 only): the k-th smallest screened distance t32 and the screening cut-off of
+    // every split whose candidate list is full
+    float k32[KMAX];
+#pragma unroll
+    for (int i = 0; i < KMAX; i++) k32[i] = INFINITY;
     float cut = INFINITY;
+    for (int s = 0; s < nsplit; s++) {
+        const size_t o = ((size_t)s * Nq + q) * KC;
+#pragma unroll
+        for (int i = 0; i < KC; i++) {
+            const int r = cand_i[o + i];
+            const float d = cand_d[o + i];
+            if (r < 0 || (self_offset >= 0 && r == self_offset + q)) continue;
+            if (d < k32[k - 1]) {  // sorted insert into the k smallest
+                float v = d;
+                for (int j = 0; j < k; j++) {
+                    const float lo = fminf(v, k32[j]);
+                    v = fmaxf(v, k32[j]);
+                    k32[j] = lo;
+                }
+            }
+        }
+        if (cand_i[o + KC - 1] >= 0) cut = fminf(cut, cand_d[o + KC - 1]);
+    }
+    // pass 2: fp64 re-rank (sklearn's own distance) of the candidates that can still be among the
+    // k nearest: a candidate with d - err(d) > t32 + err(t32) is farther (in fp64) than the k
+    // candidates at or below t32
+    const double t32 = (double)k32[k - 1];
+    const double keep = t32 < INFINITY ? t32 + err(t32) : INFINITY;
     for (int s = 0; s < nsplit; s++) {
         const size_t o = ((size_t)s * Nq + q) * KC;
         for (int i = 0; i < KC; i++) {
             const int r = cand_i[o + i];
-            if (r < 0) continue;
-            if (self_offset >= 0 && r == self_offset + q) continue;
+            const double d = (double)cand_d[o + i];
+            if (r < 0 || (self_offset >= 0 && r == self_offset + q)) continue;
+            if (d - err(d) > keep) continue;
             topk64_insert<KMAX>(dl, il, k, rdist64(qx, ref + (int64_t)r * D, D), r);
         }
-        if (cand_i[o + KC - 1] >= 0) cut = fminf(cut, cand_d[o + KC - 1]);
     }
     // certification: any row that was screened out has fp32 distance >= cut; its true fp64
     // squared distance is >= cut - tol (fp32 rounding of inputs and of the sum).
-    const double rmax = (double)__uint_as_float(*maxnorm_bits);
-    const double tol = 2e-6 * (double)cut + 1e-6 * (qn + rmax) + 1e-30;
+    const double tol = err((double)cut);
     const bool ok = !(cut < INFINITY) || ((double)cut - tol > dl[k - 1]);
     if (!ok) {
         const int slot = atomicAdd(fb_count, 1);
@@ -334,6 +393,7 @@ namespace {
 struct KnnLayout {
     size_t ref32, q32, cand_d, cand_i, misc, total;
     int DP, KC, nsplit;
+    bool exp;  // expanded-form screening (a spare padded column holds |r|^2)
 };
 
 int pick_kc(int k)
@@ -348,7 +408,14 @@ int pick_kc(int k)
 int pick_nsplit(int64_t Nr, int64_t Nq)
 {
     const int64_t qblocks = (Nq + dsp::KNN_TQ - 1) / dsp::KNN_TQ;
-    int64_t s = (2048 + qblocks - 1) / qblocks;           // aim for >= 2048 workgroups
+    // Enough workgroups to fill the chip (two per CU), as few reference splits as that allows:
+    // a longer split makes a screened distance that enters its top list rarer (~KC / rows seen),
+    // and a wave pays for an insertion whenever any of its 64 lanes makes one
+    static const int target = [] {
+        const char *e = getenv("DSP_KNN_TARGET_WGS");
+        return e ? atoi(e) : 512;
+    }();
+    int64_t s = (target + qblocks - 1) / qblocks;
     const int64_t maxs = (Nr + dsp::KNN_TR - 1) / dsp::KNN_TR;  // >= one tile per split
     if (s > maxs) s = maxs;
     if (s > 64) s = 64;
@@ -362,6 +429,7 @@ KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
 {
     KnnLayout l;
     l.DP = D <= 16 ? 16 : 32;
+    l.exp = D < l.DP;
     l.KC = pick_kc(k);
     l.nsplit = pick_nsplit(Nr, Nq);
     size_t o = 0;
@@ -375,11 +443,15 @@ KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
 }
 
 template <int DP, int KC>
-void launch_screen(dim3 g, hipStream_t s, const float *r, int64_t Nr, const float *q, int64_t Nq,
+void launch_screen(dim3 g, hipStream_t s, bool exp, const float *r, int64_t Nr, const float *q, int64_t Nq,
                    int64_t self, int nsplit, float *cd, int *ci)
 {
-    hipLaunchKernelGGL((dsp::knn_screen<DP, KC>), g, dim3(dsp::KNN_TQ), 0, s, r, Nr, q, Nq, self,
-                       nsplit, cd, ci);
+    if (exp)
+        hipLaunchKernelGGL((dsp::knn_screen<DP, KC, true>), g, dim3(dsp::KNN_TQ), 0, s, r, Nr, q, Nq, self,
+                           nsplit, cd, ci);
+    else
+        hipLaunchKernelGGL((dsp::knn_screen<DP, KC, false>), g, dim3(dsp::KNN_TQ), 0, s, r, Nr, q, Nq, self,
+                           nsplit, cd, ci);
 }
 
 template <int KC>
@@ -424,12 +496,12 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
     const int cb = 256;
     if (Nr > 0)
         hipLaunchKernelGGL(dsp::knn_convert, dim3((unsigned)((Nr + cb - 1) / cb)), dim3(cb), 0, s,
-                           ref, Nr, D, l.DP, ref32, mx);
+                           ref, Nr, D, l.DP, l.exp ? 1 : 0, ref32, mx);
     hipLaunchKernelGGL(dsp::knn_convert, dim3((unsigned)((Nq + cb - 1) / cb)), dim3(cb), 0, s,
-                       query, Nq, D, l.DP, q32, (unsigned *)nullptr);
+                       query, Nq, D, l.DP, l.exp ? 2 : 0, q32, (unsigned *)nullptr);
     const dim3 g((unsigned)((Nq + dsp::KNN_TQ - 1) / dsp::KNN_TQ), (unsigned)l.nsplit);
 #define DSP_SCREEN(DPV, KCV)                                                                  \
-    if (l.DP == DPV && l.KC == KCV) launch_screen<DPV, KCV>(g, s, ref32, Nr, q32, Nq, self_offset, \
+    if (l.DP == DPV && l.KC == KCV) launch_screen<DPV, KCV>(g, s, l.exp, ref32, Nr, q32, Nq, self_offset, \
                                                             l.nsplit, cd, ci)
     DSP_SCREEN(16, 8); DSP_SCREEN(16, 16); DSP_SCREEN(16, 24); DSP_SCREEN(16, 36);
     DSP_SCREEN(32, 8); DSP_SCREEN(32, 16); DSP_SCREEN(32, 24); DSP_SCREEN(32, 36);
