@@ -28,7 +28,11 @@ namespace dsp {
 static constexpr int KNN_TQ = 256;   // queries per screening workgroup (one per thread)
 static constexpr int KNN_TR = 256;   // reference rows per LDS tile
 static constexpr int KNN_SLACK = 3;  // extra screened candidates per split (k = 5 -> 8)
-static constexpr int KNN_RU = 4;     // reference rows per unrolled step of the screen
+static constexpr int KNN_RU = 4;     // rows x queries per unrolled step of the screen
+#ifndef DSP_KNN_QP
+#define DSP_KNN_QP 2
+#endif
+static constexpr int KNN_QP = DSP_KNN_QP;  // queries per screening thread
 
 // mode 0: plain rows (v, 0 ...); mode 1 (reference, expanded form): (-2 v, 0 ..., |v|^2);
 // mode 2 (query, expanded form): (v, 0 ..., 1) -- so that |q - r|^2 = |q|^2 + q'.r'
@@ -56,30 +60,28 @@ __global__ void knn_convert(const double *__restrict__ src, int64_t N, int D, in
     if ((threadIdx.x & 63) == 0 && maxnorm_bits) atomicMax(maxnorm_bits, __float_as_uint(nrm));
 }
 
-// insert (d, r) into the ascending list (dl, il) of length KC if it beats the last entry
+// insert (d, r) into the ascending list (dl, il) of length KC if it beats the last entry:
+// branch-free, dl'[i] = med3(dl[i-1], d, dl[i]) (an entry shifts down, takes d, or stays)
 template <int KC>
 __device__ __forceinline__ void topk_insert(float (&dl)[KC], int (&il)[KC], float d, int r)
 {
     if (!(d < dl[KC - 1])) return;
+    bool c[KC];
+#pragma unroll
+    for (int i = 0; i < KC; i++) c[i] = d < dl[i];
 #pragma unroll
     for (int i = KC - 1; i > 0; i--) {
-        const bool shift = d < dl[i - 1];
-        const bool here = !shift && d < dl[i];
-        if (shift) {
-            dl[i] = dl[i - 1];
-            il[i] = il[i - 1];
-        } else if (here) {
-            dl[i] = d;
-            il[i] = r;
-        }
+        il[i] = c[i - 1] ? il[i - 1] : (c[i] ? r : il[i]);
+        dl[i] = __builtin_amdgcn_fmed3f(dl[i - 1], d, dl[i]);
     }
-    if (d < dl[0]) {
-        dl[0] = d;
-        il[0] = r;
-    }
+    il[0] = c[0] ? r : il[0];
+    dl[0] = fminf(d, dl[0]);
 }
 
-template <int DP, int KC, bool EXP>
+// QP queries per thread (queries q0 + tid + KNN_TQ * p): every 16-B LDS read of a reference row
+// feeds QP FMAs -- a broadcast ds_read_b128 costs the CU's LDS pipe 4 cycles, shared by 4 SIMDs,
+// so at one query per thread the screen is LDS-bound
+template <int DP, int KC, bool EXP, int QP>
 __global__ __launch_bounds__(KNN_TQ) void knn_screen(const float *__restrict__ ref32, int64_t Nr,
                                                       const float *__restrict__ q32, int64_t Nq,
                                                       int64_t self_offset, int nsplit,
@@ -89,22 +91,26 @@ __global__ __launch_bounds__(KNN_TQ) void knn_screen(const float *__restrict__ r
     __shared__ __attribute__((aligned(16))) float tile[KNN_TR * DP];
     const int qb = blockIdx.x, sp = blockIdx.y;
     const int tid = threadIdx.x;
-    const int64_t q = (int64_t)qb * KNN_TQ + tid;
     const int64_t per = (Nr + nsplit - 1) / nsplit;
     const int64_t r0 = (int64_t)sp * per, r1 = min(Nr, r0 + per);
-    float qv[DP];
+    int64_t q[QP], self[QP];
+    float qv[QP][DP], qn[QP];
+    float dl[QP][KC];
+    int il[QP][KC];
 #pragma unroll
-    for (int c = 0; c < DP; c++) qv[c] = q < Nq ? q32[q * DP + c] : 0.f;
-    float qn = 0.f;  // expanded form: |q|^2 + sum q'_c r'_c, one FMA per dimension
+    for (int p = 0; p < QP; p++) {
+        q[p] = (int64_t)qb * KNN_TQ * QP + tid + KNN_TQ * p;
 #pragma unroll
-    for (int c = 0; c < DP - 1; c++) qn = fmaf(qv[c], qv[c], qn);
-    const int64_t self = (self_offset >= 0 && q < Nq) ? self_offset + q : -1;
-    float dl[KC];
-    int il[KC];
+        for (int c = 0; c < DP; c++) qv[p][c] = q[p] < Nq ? q32[q[p] * DP + c] : 0.f;
+        qn[p] = 0.f;  // expanded form: |q|^2 + sum q'_c r'_c, one FMA per dimension
 #pragma unroll
-    for (int i = 0; i < KC; i++) {
-        dl[i] = INFINITY;
-        il[i] = -1;
+        for (int c = 0; c < DP - 1; c++) qn[p] = fmaf(qv[p][c], qv[p][c], qn[p]);
+        self[p] = (self_offset >= 0 && q[p] < Nq) ? self_offset + q[p] : -1;
+#pragma unroll
+        for (int i = 0; i < KC; i++) {
+            dl[p][i] = INFINITY;
+            il[p][i] = -1;
+        }
     }
     for (int64_t t0 = r0; t0 < r1; t0 += KNN_TR) {
         const int nt = (int)min((int64_t)KNN_TR, r1 - t0);
@@ -117,45 +123,54 @@ __global__ __launch_bounds__(KNN_TQ) void knn_screen(const float *__restrict__ r
             reinterpret_cast<float4 *>(tile)[e] = v;
         }
         __syncthreads();
-        // rows in groups of KNN_RU: independent FMA chains, then the inserts in row order
-        for (int j0 = 0; j0 < nt; j0 += KNN_RU) {
-            float d[KNN_RU];
+        // rows in groups of RU: independent FMA chains, then the inserts in row order
+        constexpr int RU = KNN_RU / QP > 0 ? KNN_RU / QP : 1;
+        for (int j0 = 0; j0 < nt; j0 += RU) {
+            float d[RU][QP];
 #pragma unroll
-            for (int u = 0; u < KNN_RU; u++) {
+            for (int u = 0; u < RU; u++) {
                 const float4 *rv = reinterpret_cast<const float4 *>(tile + (j0 + u) * DP);  // rows >= nt are zero
-                d[u] = EXP ? qn : 0.f;
+#pragma unroll
+                for (int p = 0; p < QP; p++) d[u][p] = EXP ? qn[p] : 0.f;
 #pragma unroll
                 for (int c4 = 0; c4 < DP / 4; c4++) {
                     const float4 r = rv[c4];
-                    if (EXP) {
-                        d[u] = fmaf(qv[4 * c4 + 0], r.x, d[u]);
-                        d[u] = fmaf(qv[4 * c4 + 1], r.y, d[u]);
-                        d[u] = fmaf(qv[4 * c4 + 2], r.z, d[u]);
-                        d[u] = fmaf(qv[4 * c4 + 3], r.w, d[u]);
-                    } else {
-                        float t;
-                        t = qv[4 * c4 + 0] - r.x; d[u] = fmaf(t, t, d[u]);
-                        t = qv[4 * c4 + 1] - r.y; d[u] = fmaf(t, t, d[u]);
-                        t = qv[4 * c4 + 2] - r.z; d[u] = fmaf(t, t, d[u]);
-                        t = qv[4 * c4 + 3] - r.w; d[u] = fmaf(t, t, d[u]);
+#pragma unroll
+                    for (int p = 0; p < QP; p++) {
+                        if (EXP) {
+                            d[u][p] = fmaf(qv[p][4 * c4 + 0], r.x, d[u][p]);
+                            d[u][p] = fmaf(qv[p][4 * c4 + 1], r.y, d[u][p]);
+                            d[u][p] = fmaf(qv[p][4 * c4 + 2], r.z, d[u][p]);
+                            d[u][p] = fmaf(qv[p][4 * c4 + 3], r.w, d[u][p]);
+                        } else {
+                            float t;
+                            t = qv[p][4 * c4 + 0] - r.x; d[u][p] = fmaf(t, t, d[u][p]);
+                            t = qv[p][4 * c4 + 1] - r.y; d[u][p] = fmaf(t, t, d[u][p]);
+                            t = qv[p][4 * c4 + 2] - r.z; d[u][p] = fmaf(t, t, d[u][p]);
+                            t = qv[p][4 * c4 + 3] - r.w; d[u][p] = fmaf(t, t, d[u][p]);
+                        }
                     }
                 }
             }
 #pragma unroll
-            for (int u = 0; u < KNN_RU; u++) {
+            for (int u = 0; u < RU; u++) {
                 const int64_t r = t0 + j0 + u;
-                if (j0 + u < nt && r != self) topk_insert<KC>(dl, il, d[u], (int)r);
+#pragma unroll
+                for (int p = 0; p < QP; p++)
+                    if (j0 + u < nt && r != self[p]) topk_insert<KC>(dl[p], il[p], d[u][p], (int)r);
             }
         }
     }
-    if (q < Nq) {
-        const size_t o = ((size_t)sp * Nq + q) * KC;
 #pragma unroll
-        for (int i = 0; i < KC; i++) {
-            cand_d[o + i] = dl[i];
-            cand_i[o + i] = il[i];
+    for (int p = 0; p < QP; p++)
+        if (q[p] < Nq) {
+            const size_t o = ((size_t)sp * Nq + q[p]) * KC;
+#pragma unroll
+            for (int i = 0; i < KC; i++) {
+                cand_d[o + i] = dl[p][i];
+                cand_i[o + i] = il[p][i];
+            }
         }
-    }
 }
 
 #pragma clang fp contract(off)
@@ -407,7 +422,7 @@ int pick_kc(int k)
 
 int pick_nsplit(int64_t Nr, int64_t Nq)
 {
-    const int64_t qblocks = (Nq + dsp::KNN_TQ - 1) / dsp::KNN_TQ;
+    const int64_t qblocks = (Nq + dsp::KNN_TQ * dsp::KNN_QP - 1) / (dsp::KNN_TQ * dsp::KNN_QP);
     // Enough workgroups to fill the chip (two per CU), as few reference splits as that allows:
     // a longer split makes a screened distance that enters its top list rarer (~KC / rows seen),
     // and a wave pays for an insertion whenever any of its 64 lanes makes one
@@ -447,11 +462,11 @@ void launch_screen(dim3 g, hipStream_t s, bool exp, const float *r, int64_t Nr, 
                    int64_t self, int nsplit, float *cd, int *ci)
 {
     if (exp)
-        hipLaunchKernelGGL((dsp::knn_screen<DP, KC, true>), g, dim3(dsp::KNN_TQ), 0, s, r, Nr, q, Nq, self,
-                           nsplit, cd, ci);
+        hipLaunchKernelGGL((dsp::knn_screen<DP, KC, true, dsp::KNN_QP>), g, dim3(dsp::KNN_TQ), 0, s, r, Nr, q,
+                           Nq, self, nsplit, cd, ci);
     else
-        hipLaunchKernelGGL((dsp::knn_screen<DP, KC, false>), g, dim3(dsp::KNN_TQ), 0, s, r, Nr, q, Nq, self,
-                           nsplit, cd, ci);
+        hipLaunchKernelGGL((dsp::knn_screen<DP, KC, false, dsp::KNN_QP>), g, dim3(dsp::KNN_TQ), 0, s, r, Nr, q,
+                           Nq, self, nsplit, cd, ci);
 }
 
 template <int KC>
@@ -499,7 +514,7 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
                            ref, Nr, D, l.DP, l.exp ? 1 : 0, ref32, mx);
     hipLaunchKernelGGL(dsp::knn_convert, dim3((unsigned)((Nq + cb - 1) / cb)), dim3(cb), 0, s,
                        query, Nq, D, l.DP, l.exp ? 2 : 0, q32, (unsigned *)nullptr);
-    const dim3 g((unsigned)((Nq + dsp::KNN_TQ - 1) / dsp::KNN_TQ), (unsigned)l.nsplit);
+    const dim3 g((unsigned)((Nq + dsp::KNN_TQ * dsp::KNN_QP - 1) / (dsp::KNN_TQ * dsp::KNN_QP)), (unsigned)l.nsplit);
 #define DSP_SCREEN(DPV, KCV)                                                                  \
     if (l.DP == DPV && l.KC == KCV) launch_screen<DPV, KCV>(g, s, l.exp, ref32, Nr, q32, Nq, self_offset, \
                                                             l.nsplit, cd, ci)
