@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step from Python instead of replaying a captured HIP graph")
+    ap.add_argument("--knn-ref", type=int, default=100000,
+                    help="KNN leg (BASELINE configs[4]): reference rows, all of them queried (0: skip)")
+    ap.add_argument("--knn-k", type=int, default=5)
     return ap.parse_args()
 
 
@@ -139,6 +142,7 @@ def main():
     else:
         total_frames = my_frames
         ag_ms = None
+    knn = knn_leg(args, dev, world) if args.knn_ref > 0 else None
 
     result = None
     if rank == 0:
@@ -180,12 +184,59 @@ def main():
         }
         if ag_ms is not None:
             result["allgather_feat_ms"] = round(ag_ms, 4)
+        if knn is not None:
+            result["knn"] = knn
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(host[0], L, S, args.window, vad, args.cpu_seconds)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return result
+
+
+def knn_leg(args, dev, world):
+    """BASELINE configs[4] beside the headline metric: exact k-NN (KNeighborsClassifier
+    semantics) of every one of --knn-ref synthetic z-scored 15-d vectors against all of them
+    (self excluded), queries sharded over the ranks, results gathered (RCCL all-gather).  Not
+    part of ``value``; reported as its own object with its VALU roofline (45 flop per pair)."""
+    import torch
+    import torch.distributed as dist
+    from src.distributed import knn_sharded
+    from src.pipeline import knn_classify
+    rng = np.random.default_rng(0)  # same reference set on every rank
+    n, dim = args.knn_ref, 15
+    centres = rng.standard_normal((10, dim)) * 1.5
+    y = rng.integers(0, 10, n).astype(np.int32)
+    X = centres[y] + rng.standard_normal((n, dim))
+    X = (X - X.mean(0)) / X.std(0)
+    Xd, yd = torch.as_tensor(X, device=dev), torch.as_tensor(y, device=dev)
+    knn_sharded(knn_classify, Xd, yd, Xd, args.knn_k, self_query=True)  # warm-up
+    torch.cuda.synchronize(dev)
+    ts = []
+    for _ in range(3):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        idx, dd, pred = knn_sharded(knn_classify, Xd, yd, Xd, args.knn_k, self_query=True)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    if world > 1:
+        tt = torch.tensor([t], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = tt.item()
+    pairs = float(n) * n
+    tf = pairs * 45 / t / 1e12
+    return {"metric": "k-NN pairs/s (15-d, exact, k=%d, self-query, gathered)" % args.knn_k,
+            "value": round(pairs / t, 1), "unit": "pairs/s", "ms": round(t * 1e3, 4),
+            "ref": n, "queries": n, "queries_per_rank": -(-n // world),
+            "roofline": {"bound": "valu", "achieved": round(tf, 2), "peak": 157.3 * world, "unit": "TFLOP/s",
+                         "frac": round(tf / (157.3 * world), 4), "flop_per_pair": 45,
+                         "note": "whole-job wall time incl. conversion, merge and the result all-gather"},
+            "data": "synthetic z-scored 15-d vectors around 10 class centres"}
 
 
 def cpu_baseline(batch, L, S, window, vad, budget_s):
