@@ -1481,14 +1481,15 @@ __device__ __forceinline__ Ctx make_ctx(const ExtractParams &p, unsigned char *l
 }
 
 // the rare near-tie redo, compiled out of line so its exact-order machinery does not weigh on
-// the register allocation of the streaming path
-// The kernel arguments are read in place from the kernel-argument segment: passing them by value
-// would copy the struct to scratch at every kernel entry (all lanes of every wave, ~24 MB of HBM
-// writes per 1000-clip launch).
+// the register allocation of the streaming path.  It reads the kernel arguments where the kernel
+// received them: the kernel passes its kernarg-segment pointer (ExtractParams is the first
+// argument).  Passing the struct itself, by value or by reference, makes the kernel copy it to
+// scratch in every lane at entry (~24-60 MB of HBM writes per 1000-clip launch), and
+// __builtin_amdgcn_kernarg_segment_ptr() is null inside a called function.
 template <bool FAST>
-__device__ __attribute__((noinline)) void clip_exact(int i)
+__device__ __attribute__((noinline)) void clip_exact(const ExtractParams *pk, int i)
 {
-    const ExtractParams &p = *(const ExtractParams *)__builtin_amdgcn_kernarg_segment_ptr();
+    const ExtractParams &p = *pk;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     Ctx c = make_ctx<FAST>(p, lds);
     c.stamp_clip = i;
@@ -1580,7 +1581,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     const int nd = sh->ndefer;
     for (int d = 0; d < nd; d++) {
         const int j = c.defer[d];
-        clip_exact<FAST>(j);
+        clip_exact<FAST>((const ExtractParams *)__builtin_amdgcn_kernarg_segment_ptr(), j);
         __syncthreads();
     }
     WG_STAMP(22);

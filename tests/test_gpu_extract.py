@@ -178,9 +178,10 @@ def test_tied_vad_energies():
 
 def test_near_tie_redo_exact():
     """An endpoint energy exactly at the high threshold: most frames are a +-A square wave
-    (energy P, so p90 = P and T1 = P / 2) and a stretch of (+A, -A, 0, 0) gives frames of energy
-    exactly P / 2 = T1 (mean 0 throughout, so the energies are exact).  The certified decision
-    flags the near tie and the clip is redone in numpy's exact float64 order (clip_exact)."""
+    (energy P, so p90 = P and T1 = P / 2) and the clip opens with (+A, -A, 0, 0), frames of energy
+    exactly P / 2 = T1 (mean 0 throughout, so the energies are exact).  The first-frame-above-T1
+    decision depends on them: the certified scan flags the near tie and the clip is redone in
+    numpy's exact float64 order (clip_exact)."""
     import torch
     from src.pipeline import FeatureExtractor, create_window
     for L, S in [(1000, 400), (1102, 441)]:
@@ -188,11 +189,10 @@ def test_near_tie_redo_exact():
         A = 3000
         x = np.empty(n, np.int64)
         x[0::2], x[1::2] = A, -A
-        pat = np.tile(np.array([A, -A, 0, 0]), 1000)
-        x[20000:24000] = pat
+        x[:4000] = np.tile(np.array([A, -A, 0, 0]), 1000)
         clip = x.astype(np.int16)
         other = clip.copy()
-        other[30000:30100] = 0  # a second clip in the same launch that needs no redo
+        other[:4000] = other[4000:8000]  # a second clip in the same launch that needs no redo
         clips = [clip, other]
         off = np.arange(len(clips) + 1, dtype=np.int64) * n
         pcm = np.concatenate(clips)
@@ -205,5 +205,5 @@ def test_near_tie_redo_exact():
             assert tuple(out["start_end"][i]) == (r["start"], r["end"]), (L, i)
             assert out["n_frames"][i] == r["n_frames"], (L, i)
             assert not feat_close(out["feat"][i], r["feat"]).any(), (L, i)
-        # the tie was seen and redone exactly
-        assert out["status"][0] & 0x100, out["status"]
+        if L == 1000:  # frames 0-7 at exactly T1 decide N3: the tie was seen and redone exactly
+            assert out["status"][0] & 0x100, out["status"]
