@@ -2,8 +2,9 @@
 
 ``load_dataset`` keeps the reference's dataset contract (class = index of the sorted
 sub-directory name, files in glob order, errored files skipped: run_experiments.py:64-111) but
-reads every WAV first and extracts all of them in one fused kernel launch per window type
-instead of one Python loop iteration per file.  ``experiment_classifier_comparison`` /
+decodes every WAV once (src/dataset.PCMDataset: host threads, one pinned upload) and extracts all
+of them in one fused kernel launch per window type instead of one Python loop iteration per
+file; the window comparison reuses the HBM-resident PCM.  ``experiment_classifier_comparison`` /
 ``experiment_window_comparison`` follow :249-393 with the KNN on the device and the other
 scikit-learn classifiers unchanged; plots (src/visualization.py) and the MLP are out of scope,
 results are written as JSON.
@@ -11,7 +12,6 @@ results are written as JSON.
 import json
 import os
 import sys
-from glob import glob
 
 import numpy as np
 
@@ -20,21 +20,10 @@ if PKG not in sys.path:
     sys.path.insert(0, PKG)
 
 import config  # noqa: E402
-from src.audio_processing import load_wav_pcm  # noqa: E402
+from src.dataset import PCMDataset, list_dataset  # noqa: E402,F401
 from src.feature_extraction import normalize_features  # noqa: E402
 from src.models import create_classifier  # noqa: E402
-from src.pipeline import FEATURE_NAMES, FeatureExtractor  # noqa: E402
-
-
-def list_dataset(data_dir):
-    """[(path, class_index)] in the reference's order, and the class names."""
-    classes = sorted(d for d in os.listdir(data_dir)
-                     if os.path.isdir(os.path.join(data_dir, d)) and not d.startswith('.'))
-    files = []
-    for ci, name in enumerate(classes):
-        for f in glob(os.path.join(data_dir, name, '*.wav')):
-            files.append((f, ci))
-    return files, classes
+from src.pipeline import FEATURE_NAMES  # noqa: E402
 
 
 class SpeechRecognitionExperiment:
@@ -46,35 +35,18 @@ class SpeechRecognitionExperiment:
         self.y = None
         self.feature_names = None
         self.skipped = []
+        self._data = None  # PCMDataset, decoded once per runner
 
     def load_dataset(self, window_type='hamming', do_endpoint_detection=True):
         """-> X [n, 15] float64, y [n], feature_names (run_experiments.py:45-126)."""
-        files, self.class_names = list_dataset(self.data_dir)
-        clips, labels, self.skipped = [], [], []
-        for path, ci in files:
-            try:
-                pcm, _ = load_wav_pcm(path)
-            except Exception as e:  # the reference skips files it cannot process (:109-111)
-                self.skipped.append((path, str(e)))
-                continue
-            clips.append(pcm)
-            labels.append(ci)
-        if not clips:
-            raise ValueError("no readable WAV files under %s" % self.data_dir)
-        lens = np.array([c.size for c in clips], dtype=np.int64)
-        off = np.zeros(len(clips) + 1, dtype=np.int64)
-        off[1:] = np.cumsum(lens)
-        pcm = np.concatenate(clips + [np.zeros(8, np.int16)])
-        fx = FeatureExtractor(config.FRAME_LENGTH, config.FRAME_SHIFT, window_type, do_endpoint_detection,
-                              config.ENERGY_HIGH_RATIO, config.ENERGY_LOW_RATIO, config.ZCR_THRESHOLD_RATIO)
-        out = fx(pcm, off, max_len=int(lens.max()))
-        feat = out["feat"].cpu().numpy().astype(np.float64)
-        status = out["status"].cpu().numpy() & 0xFF
-        keep = status == 0
-        for j in np.nonzero(~keep)[0]:
-            self.skipped.append((files[j][0], "status %d" % status[j]))
-        self.X = feat[keep]
-        self.y = np.asarray(labels)[keep]
+        if self._data is None:
+            self._data = PCMDataset(self.data_dir)
+            self.class_names = self._data.class_names
+        d = self._data
+        X, y, ok = d.extract(config.FRAME_LENGTH, config.FRAME_SHIFT, window_type, do_endpoint_detection,
+                             config.ENERGY_HIGH_RATIO, config.ENERGY_LOW_RATIO, config.ZCR_THRESHOLD_RATIO)
+        self.skipped = list(d.skipped) + [(d.files[j][0], "processing failed") for j in np.nonzero(~ok)[0]]
+        self.X, self.y = X, y
         self.feature_names = list(FEATURE_NAMES)
         return self.X, self.y, self.feature_names
 

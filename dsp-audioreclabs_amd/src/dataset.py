@@ -1,0 +1,168 @@
+"""Dataset side of the hot path: WAV decoding off the Python
+per-file loop, one pinned host->device upload, and every (frame length, frame shift, window)
+configuration extracted from the same HBM-resident PCM.
+
+The reference decodes and processes one file per loop iteration for every configuration it
+evaluates (train_model.py:21-110 inside ablation_study.py:146-163, 230-247;
+experiments/run_experiments.py:78-111 once per window type).  Here a dataset is decoded once,
+in parallel threads (``load_wav_pcm`` is file I/O plus numpy, both of which release the GIL),
+packed into one int16 buffer with int64 offsets, uploaded once, and each configuration is one
+fused kernel launch over all clips (``FeatureExtractor``).  ``iter_device_batches`` is the
+streaming form for file lists larger than host or device memory: batch k+1 is decoded and copied
+on a side stream while batch k is being processed.
+"""
+import os
+from concurrent.futures import ThreadPoolExecutor
+from glob import glob
+
+import numpy as np
+
+from .audio_processing import load_wav_pcm
+from .pipeline import FeatureExtractor
+
+
+def list_dataset(data_dir):
+    """[(path, class_index)] and the class names, in the reference's order: class = index of the
+    sorted sub-directory name, files in glob order (run_experiments.py:64-82, train_model.py:56-71)."""
+    classes = sorted(d for d in os.listdir(data_dir)
+                     if os.path.isdir(os.path.join(data_dir, d)) and not d.startswith('.'))
+    files = []
+    for ci, name in enumerate(classes):
+        for f in glob(os.path.join(data_dir, name, '*.wav')):
+            files.append((f, ci))
+    return files, classes
+
+
+def _decode(paths, n_threads):
+    """[(int16 pcm or None, error or None)] in input order."""
+    def one(p):
+        try:
+            return load_wav_pcm(p)[0], None
+        except Exception as e:  # the reference skips files it cannot process (:109-111)
+            return None, str(e)
+    if n_threads <= 1 or len(paths) < 2:
+        return [one(p) for p in paths]
+    with ThreadPoolExecutor(max_workers=n_threads) as ex:
+        return list(ex.map(one, paths))
+
+
+def pack_clips(clips):
+    """int16 clips -> (packed int16 [sum + 8], offsets int64 [B+1]); the 8-sample tail keeps the
+    last clip's 16-B vectors inside the buffer."""
+    lens = np.array([c.size for c in clips], dtype=np.int64)
+    off = np.zeros(len(clips) + 1, dtype=np.int64)
+    off[1:] = np.cumsum(lens)
+    return np.concatenate(list(clips) + [np.zeros(8, np.int16)]), off
+
+
+def _upload(pcm, off, device, stream=None):
+    """Pinned staging + asynchronous copy on ``stream`` (current stream if None)."""
+    import torch
+    hp = torch.from_numpy(pcm).pin_memory()
+    ho = torch.from_numpy(off).pin_memory()
+    if stream is None:
+        return hp.to(device, non_blocking=True), ho.to(device, non_blocking=True), (hp, ho)
+    with torch.cuda.stream(stream):
+        return hp.to(device, non_blocking=True), ho.to(device, non_blocking=True), (hp, ho)
+
+
+def _threads(n_threads):
+    if n_threads:
+        return int(n_threads)
+    try:
+        return max(1, min(16, len(os.sched_getaffinity(0))))
+    except AttributeError:
+        return max(1, min(16, os.cpu_count() or 1))
+
+
+class PCMDataset:
+    """A directory of class sub-directories of WAV files, decoded once and resident in HBM.
+
+    Attributes: ``pcm`` int16 and ``offsets`` int64 device tensors (all readable clips back to
+    back), ``labels`` int array, ``files`` [(path, class)] of the kept clips, ``skipped``
+    [(path, reason)], ``class_names``.
+    """
+
+    def __init__(self, data_dir, n_threads=None, device=None):
+        from . import _hip
+        self.device = device or _hip.require_device()
+        files, self.class_names = list_dataset(data_dir)
+        decoded = _decode([f for f, _ in files], _threads(n_threads))
+        clips, self.files, self.skipped = [], [], []
+        for (path, ci), (pcm, err) in zip(files, decoded):
+            if pcm is None or pcm.size == 0:
+                self.skipped.append((path, err or "empty file"))
+                continue
+            clips.append(pcm)
+            self.files.append((path, ci))
+        if not clips:
+            raise ValueError("no readable WAV files under %s" % data_dir)
+        self.labels = np.array([ci for _, ci in self.files], dtype=np.int64)
+        pcm, off = pack_clips(clips)
+        self.max_len = int(np.diff(off).max())
+        self.pcm, self.offsets, self._pinned = _upload(pcm, off, self.device)
+
+    def __len__(self):
+        return len(self.files)
+
+    def extract(self, frame_length, frame_shift, window_type='hamming', do_endpoint_detection=True,
+                energy_high_ratio=0.5, energy_low_ratio=0.1, zcr_threshold_ratio=1.5):
+        """One fused launch over every clip -> (X float64 [n_ok, 15], y [n_ok], ok mask [n]).
+
+        Clips whose processing the reference would abandon with a ValueError (status & 0xFF != 0)
+        are dropped, as the reference's loaders skip them (train_model.py:91-94)."""
+        fx = FeatureExtractor(frame_length, frame_shift, window_type, do_endpoint_detection,
+                              energy_high_ratio, energy_low_ratio, zcr_threshold_ratio, device=self.device)
+        out = fx(self.pcm, self.offsets, max_len=self.max_len)
+        feat = out["feat"].cpu().numpy().astype(np.float64)
+        ok = (out["status"].cpu().numpy() & 0xFF) == 0
+        return feat[ok], self.labels[ok], ok
+
+    def sweep(self, configs, **kw):
+        """Feature matrices for several (frame_length, frame_shift, window_type) configurations
+        over the same resident PCM: {config: (X, y, ok)}."""
+        return {tuple(c): self.extract(*c, **kw) for c in configs}
+
+
+def iter_device_batches(paths, batch_clips, n_threads=None, device=None):
+    """Stream a file list through the device in batches: yields (pcm, offsets, max_len, index
+    list, skipped) with the device tensors of batch k ready while batch k+1 is decoded on host
+    threads and copied on a side stream (the consumer's launches on the current stream overlap
+    the next copy).  Paths that fail to decode are reported in ``skipped`` and not in the batch."""
+    import torch
+    from . import _hip
+    device = device or _hip.require_device()
+    copy_stream = torch.cuda.Stream(device)
+    nt = _threads(n_threads)
+    pool = ThreadPoolExecutor(max_workers=1)
+
+    def prepare(lo):
+        idx = list(range(lo, min(lo + batch_clips, len(paths))))
+        dec = _decode([paths[i] for i in idx], nt)
+        keep = [(i, p) for i, (p, e) in zip(idx, dec) if p is not None and p.size > 0]
+        skipped = [(paths[i], e or "empty file") for i, (p, e) in zip(idx, dec) if p is None or p.size == 0]
+        if not keep:
+            return None, [], skipped
+        pcm, off = pack_clips([p for _, p in keep])
+        dp, do, pin = _upload(pcm, off, device, copy_stream)
+        ev = torch.cuda.Event()
+        ev.record(copy_stream)
+        return (dp, do, int(np.diff(off).max()), ev, pin), [i for i, _ in keep], skipped
+
+    try:
+        fut = pool.submit(prepare, 0)
+        for lo in range(0, len(paths), batch_clips):
+            cur, idx, skipped = fut.result()
+            if lo + batch_clips < len(paths):
+                fut = pool.submit(prepare, lo + batch_clips)
+            if cur is None:
+                yield None, None, 0, idx, skipped
+                continue
+            dp, do, ml, ev, _pin = cur
+            cs = torch.cuda.current_stream(device)
+            cs.wait_event(ev)
+            dp.record_stream(cs)  # allocated on the copy stream, used on this one
+            do.record_stream(cs)
+            yield dp, do, ml, idx, skipped
+    finally:
+        pool.shutdown(wait=True)

@@ -53,3 +53,19 @@ def test_dataset_listing_order(tmp_path):
     files, classes = list_dataset(str(tmp_path))
     assert classes == ["a", "b"]
     assert [(os.path.basename(f), c) for f, c in files] == [("x.wav", 0), ("y.wav", 1)]
+
+
+def test_dataset_listing_and_packing(tmp_path):
+    """src/dataset.py host side: class = sorted sub-directory index, glob order, packed buffer
+    with an 8-sample tail and int64 offsets."""
+    from src.dataset import list_dataset, pack_clips
+    for name in ("b", "a", ".hidden"):
+        (tmp_path / name).mkdir()
+    (tmp_path / "a" / "x.wav").write_bytes(b"")
+    (tmp_path / "b" / "y.wav").write_bytes(b"")
+    (tmp_path / "b" / "notes.txt").write_bytes(b"")
+    files, classes = list_dataset(str(tmp_path))
+    assert classes == ["a", "b"] and [(os.path.basename(f), c) for f, c in files] == [("x.wav", 0), ("y.wav", 1)]
+    clips = [np.arange(5, dtype=np.int16), np.arange(3, dtype=np.int16) + 100]
+    pcm, off = pack_clips(clips)
+    assert list(off) == [0, 5, 8] and pcm.size == 16 and list(pcm[5:8]) == [100, 101, 102] and not pcm[8:].any()

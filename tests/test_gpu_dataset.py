@@ -1,0 +1,112 @@
+"""GPU tests of the dataset side (src/dataset.py, train_model.py, ablation_study.py): decode
+once, HBM-resident PCM, one fused launch per (frame length, frame shift, window) setting, and
+the streamed batch form -- each compared with the C oracle per file."""
+import json
+import os
+import wave
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _write_wav(path, data, width=2, channels=1, sr=44100):
+    with wave.open(str(path), "wb") as w:
+        w.setnchannels(channels)
+        w.setsampwidth(width)
+        w.setframerate(sr)
+        w.writeframes(np.ascontiguousarray(data).tobytes())
+
+
+def _close(a, b, tol=1e-5):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    scale = np.repeat(np.abs(b[[0, 5, 10]]), 5)
+    return np.all(np.abs(a - b) <= tol * np.abs(b) + 1e-6 * scale + 1e-30)
+
+
+@pytest.fixture()
+def dataset_dir(tmp_path):
+    from src.synth import make_clip
+    for c in range(3):
+        d = tmp_path / ("w%d" % c)
+        d.mkdir()
+        for j in range(5):
+            x = make_clip(2000 + 10 * c + j, n_samples=36000 + 1013 * j, label=c, n_classes=3)
+            if c == 2 and j == 4:  # 8-bit file: same samples >> 8, offset 128
+                _write_wav(d / ("s%d.wav" % j), ((x.astype(np.int32) >> 8) + 128).astype(np.uint8), width=1)
+            else:
+                _write_wav(d / ("s%d.wav" % j), x)
+    with wave.open(str(tmp_path / "w0" / "zz_bad.wav"), "wb") as w:  # 24-bit: the reference raises
+        w.setnchannels(1)
+        w.setsampwidth(3)
+        w.setframerate(44100)
+        w.writeframes(b"\0" * 300)
+    return str(tmp_path)
+
+
+def _oracle_rows(files, L, S, win):
+    from src.audio_processing import load_wav_pcm
+    from src.pipeline import create_window
+    w = create_window(win, L)
+    return [oracle.process_clip(load_wav_pcm(f)[0], L, S, w)["feat"] for f, _ in files]
+
+
+def test_pcm_dataset_sweep(dataset_dir):
+    from src.dataset import PCMDataset
+    d = PCMDataset(dataset_dir, n_threads=4)
+    assert len(d) == 15 and len(d.skipped) == 1 and d.skipped[0][0].endswith("zz_bad.wav")
+    assert list(d.labels) == [ci for _, ci in d.files] and d.class_names == ["w0", "w1", "w2"]
+    cfgs = [(1102, 441, "hamming"), (882, 352, "hanning"), (441, 132, "rectangular")]
+    res = d.sweep(cfgs)
+    for (L, S, win) in cfgs:
+        X, y, ok = res[(L, S, win)]
+        assert ok.all() and X.shape == (15, 15)
+        for row, ref in zip(X, _oracle_rows(d.files, L, S, win)):
+            assert _close(row, ref), (L, S, win)
+
+
+def test_train_model_and_ablation(dataset_dir, tmp_path):
+    import ablation_study
+    import train_model
+    X, y, classes, names = train_model.load_dataset(dataset_dir, frame_length_ms=20, frame_shift_ms=8,
+                                                   window_type="hamming", verbose=False)
+    d = train_model.dataset(dataset_dir)
+    assert X.shape == (15, 15) and classes == ["w0", "w1", "w2"] and names[0] == "energy_mean"
+    for row, ref in zip(X, _oracle_rows(d.files, 882, 352, "hamming")):  # int(44100 * 20 / 1000) = 882
+        assert _close(row, ref)
+    r = train_model.train_and_evaluate(X, y, "knn", test_size=0.4, verbose=False)
+    assert 0.0 <= r["accuracy"] <= 1.0 and 0.0 <= r["train_accuracy"] <= 1.0
+    out = ablation_study.ablation_frame_length(dataset_dir, [20, 25], save_dir=str(tmp_path / "fl"),
+                                               verbose=False)
+    assert sorted(out) == [20, 25]
+    saved = json.load(open(os.path.join(str(tmp_path / "fl"), "results.json")))
+    assert saved["experiment"] == "frame_length_ms" and set(saved["results"]) == {"20", "25"}
+
+
+def test_streamed_batches_match_one_launch(dataset_dir):
+    import torch
+    from src.dataset import PCMDataset, iter_device_batches, list_dataset
+    from src.pipeline import FeatureExtractor
+    files, _ = list_dataset(dataset_dir)
+    paths = [f for f, _ in files]
+    fx = FeatureExtractor(1102, 441, "hamming", True)
+    rows, skipped = {}, []
+    for pcm, off, ml, idx, sk in iter_device_batches(paths, batch_clips=4, n_threads=2):
+        skipped += sk
+        if pcm is None:
+            continue
+        feat = fx(pcm, off, max_len=ml)["feat"].cpu().numpy()
+        for r, i in enumerate(idx):
+            rows[i] = feat[r]
+    torch.cuda.synchronize()
+    assert [p for p, _ in skipped] == [p for p in paths if p.endswith("zz_bad.wav")]
+    d = PCMDataset(dataset_dir)
+    X, _, _ = d.extract(1102, 441, "hamming")
+    kept = [paths.index(f) for f, _ in d.files]
+    got = np.array([rows[i] for i in kept], np.float64)
+    # same clips at other offsets in the packed buffer: the fp32 windowed sums run over other
+    # 16-B vector boundaries, so equal within the fp32 tolerance, not bit for bit
+    assert all(_close(a, b) for a, b in zip(got, X))
