@@ -118,6 +118,31 @@ class PCMDataset:
         ok = (out["status"].cpu().numpy() & 0xFF) == 0
         return feat[ok], self.labels[ok], ok
 
+    def extract_both(self, frame_length, frame_shift, window_type='hamming', do_endpoint_detection=True,
+                     use_only_energy_zcr=True, energy_high_ratio=0.5, energy_low_ratio=0.1,
+                     zcr_threshold_ratio=1.5):
+        """compare_feature_methods.py:43-115 in one fused launch: the statistical matrix and the
+        padded sequence tensor of the same clips.
+
+        -> (X_stat float64 [n_ok, 15], y [n_ok], X_seq float64 [n_ok, max_frames, 2|3], lengths
+        [n_ok]).  The kernel writes each clip's per-frame (E, M, ZCR) rows into a zeroed
+        [B, ld, 3] buffer, so cutting it at the batch's longest sequence is exactly
+        ``pad_or_truncate_sequence(seq, max(lengths))`` (fe.py:135-154) for every clip; the
+        columns are (E, ZCR) with ``use_only_energy_zcr`` (fe.py:124-128)."""
+        fx = FeatureExtractor(frame_length, frame_shift, window_type, do_endpoint_detection,
+                              energy_high_ratio, energy_low_ratio, zcr_threshold_ratio,
+                              return_sequences=True, device=self.device)
+        out = fx(self.pcm, self.offsets, max_len=self.max_len)
+        ok = (out["status"].cpu().numpy() & 0xFF) == 0
+        import torch
+        torch_ok = torch.as_tensor(ok, device=out["seq"].device)
+        lengths = out["n_frames"].cpu().numpy().astype(np.int64)[ok]
+        width = int(lengths.max()) if lengths.size else 0
+        cols = [0, 2] if use_only_energy_zcr else [0, 1, 2]
+        seq = out["seq"][torch_ok][:, :width][:, :, cols].to(torch.float64).cpu().numpy()
+        feat = out["feat"].cpu().numpy().astype(np.float64)[ok]
+        return feat, self.labels[ok], seq, lengths
+
     def sweep(self, configs, **kw):
         """Feature matrices for several (frame_length, frame_shift, window_type) configurations
         over the same resident PCM: {config: (X, y, ok)}."""

@@ -110,3 +110,24 @@ def test_streamed_batches_match_one_launch(dataset_dir):
     # same clips at other offsets in the packed buffer: the fp32 windowed sums run over other
     # 16-B vector boundaries, so equal within the fp32 tolerance, not bit for bit
     assert all(_close(a, b) for a, b in zip(got, X))
+
+
+def test_extract_both_matches_oracle_padded(dataset_dir):
+    """compare_feature_methods.py:43-115: one launch gives the statistical rows and the padded
+    (E, ZCR) sequences; each row against the C oracle, padding rows exactly zero."""
+    from src.dataset import PCMDataset
+    from src.audio_processing import load_wav_pcm
+    from src.pipeline import create_window
+    d = PCMDataset(dataset_dir, n_threads=4)
+    X, y, seq, lengths = d.extract_both(1102, 441, "hamming")
+    assert X.shape == (15, 15) and seq.shape == (15, int(lengths.max()), 2) and list(y) == list(d.labels)
+    w = create_window("hamming", 1102)
+    for i, (f, _) in enumerate(d.files):
+        r = oracle.process_clip(load_wav_pcm(f)[0], 1102, 441, w)
+        n = int(r["n_frames"])
+        assert lengths[i] == n and _close(X[i], r["feat"])
+        np.testing.assert_array_equal(seq[i, :n, 1], r["seq"][:, 2])
+        np.testing.assert_allclose(seq[i, :n, 0], r["seq"][:, 0], rtol=1e-5, atol=1e-30)
+        assert not seq[i, n:].any()
+    _, _, seq3, _ = d.extract_both(1102, 441, "hamming", use_only_energy_zcr=False)
+    assert seq3.shape[2] == 3 and np.array_equal(seq3[:, :, [0, 2]], seq)
