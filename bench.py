@@ -2,18 +2,27 @@
 """Headline benchmark: frames/s of framing + window + E/M/ZCR (+ double-threshold VAD) on
 1 s 44.1 kHz clips (BASELINE.json "metric"), one process per GPU.
 
-Workload at N=1 is BASELINE.json configs[1]: 1000 synthetic 1 s utterances per GPU, Hamming
-window, all three features + VAD (reference defaults L=1102, S=441, config.py:39-40).  A
-"step" is one pass of the fused HIP kernel over one 1000-clip batch that is already resident
-in HBM; steps rotate over a pool of batches larger than the 256 MiB Infinity Cache so every
-step streams its input from HBM.  Frames counted per clip = VAD frames (98) + frames after the
-endpoint crop (data dependent), the same frames the reference computes E/ZCR on.
+Workload: the north-star batch, 100 000 synthetic 1 s utterances (BASELINE.json north_star and
+configs[3]; 8.8 GB of int16 PCM, which fits one GPU), Hamming window, all three features +
+VAD, reference defaults L=1102, S=441 (config.py:39-40).  The batch is sharded over the ranks
+(rank r holds shard_range(clips, r, N), generated on its own device), so N=8 is exactly
+configs[3] and the scaling is strong.  A "step" is one pass of the fused HIP kernel over the
+rank's whole shard, already resident in HBM.  Frames counted per clip = VAD frames (98) +
+frames after the endpoint crop (data dependent), the frames the reference computes E/ZCR on.
+
+Beside the metric (not part of ``value``):
+  * ``window_sweep`` -- configs[2]: 10 000 clips x {rectangular, hamming, hanning};
+  * ``allgather`` (N > 1) -- the one exchange step, all per-clip results in one RCCL all-gather;
+  * ``knn`` -- configs[4]: exact k=5 self-query over 100 000 15-d vectors, queries sharded;
+  * ``cpu_baseline`` (N = 1) -- the C restatement of the reference on this box's host cores,
+    on a bounded sample of the same clips, whose outputs are also compared with the GPU's.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -26,15 +35,15 @@ sys.path.insert(0, os.path.join(REPO, "dsp-audioreclabs_amd"))
 METRIC = "frames/sec (framing+window+E/M/ZCR) on 1 s 44.1 kHz clips; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 OUT_BYTES_PER_CLIP = 15 * 4 + 2 * 4 + 4 + 4  # feat f32[15] + start/end + n_frames + status
+LLC_BYTES = 256 << 20  # MI355X Infinity Cache
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--clips", type=int, default=1000, help="clips per GPU per step")
-    ap.add_argument("--pool", type=int, default=4, help="distinct resident batches per GPU")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--clips", type=int, default=100000, help="clips of the whole job (sharded over ranks)")
     ap.add_argument("--frame-length", type=int, default=1102)
     ap.add_argument("--frame-shift", type=int, default=441)
     ap.add_argument("--window", default="hamming")
@@ -43,10 +52,23 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every step from Python instead of replaying a captured HIP graph")
+    ap.add_argument("--sweep-clips", type=int, default=10000, help="window-sweep leg, configs[2] (0: skip)")
     ap.add_argument("--knn-ref", type=int, default=100000,
                     help="KNN leg (BASELINE configs[4]): reference rows, all of them queried (0: skip)")
     ap.add_argument("--knn-k", type=int, default=5)
     return ap.parse_args()
+
+
+def timed_launches(fn, n, stream):
+    """Mean duration (ms) of n launches of fn() by HIP events recorded on the launch stream."""
+    import torch
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize()
+    return float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
 
 def main():
@@ -63,25 +85,28 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
+    from src.distributed import gather_packed, shard_range
     from src.pipeline import FeatureExtractor
-    from src.synth import make_batch
+    from src.synth import make_batch_device
 
-    C, P, N = args.clips, args.pool, 44100
+    N = 44100
     L, S = args.frame_length, args.frame_shift
     vad = not args.no_vad
-    # each rank generates its own contiguous slice of the global clip stream (seed = index)
-    host = make_batch(P * C, base_seed=0, start=rank * P * C).reshape(P, C, N)
-    pool = torch.as_tensor(host).to(dev)
+    lo, hi = shard_range(args.clips, rank, world)
+    C = hi - lo
+    # a shard smaller than the Infinity Cache is rotated over distinct copies so that every step
+    # streams its input from HBM
+    P = max(1, math.ceil(2 * LLC_BYTES / max(1, C * 2 * N)))
+    pool = [make_batch_device(C, dev, base_seed=p, start=lo) for p in range(P)]
     fx = FeatureExtractor(L, S, args.window, vad, device=dev)
     stream = torch.cuda.current_stream(dev)
 
     # frames per batch (VAD frames + feature frames), counted from the kernel's own outputs
+    nv = ((N - L) // S + 1) if (vad and N >= L) else 0
     frames = []
     for p in range(P):
         out = fx(pool[p])
-        nf = out["n_frames"].to(torch.int64).sum().item()
-        nv = C * ((N - L) // S + 1) if (vad and N >= L) else 0
-        frames.append(nf + nv)
+        frames.append(out["n_frames"].to(torch.int64).sum().item() + nv * C)
         st = out["status"].cpu().numpy() & 0xFF
         assert not st.any(), "clip errors in benchmark batch"
     for i in range(args.warmup):
@@ -90,16 +115,10 @@ def main():
 
     K = args.steps
     # per-launch kernel time on the launch stream (HIP events), for the roofline
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
-    for i in range(K):
-        ev[i][0].record(stream)
-        fx(pool[i % P])
-        ev[i][1].record(stream)
-    torch.cuda.synchronize(dev)
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    # the timed steps: the K launches captured once into a HIP graph and replayed, so the host's
-    # per-call overhead (ctypes, Python) does not throttle a 60 us kernel; --no-graph launches
-    # each step from Python
+    kern_ms = timed_launches(lambda: fx(pool[0]), max(3, min(K, 10)), stream) if P == 1 else \
+        float(np.mean([timed_launches(lambda: fx(pool[p]), 2, stream) for p in range(P)]))
+    # the timed steps: captured once into a HIP graph and replayed, so host overhead (ctypes,
+    # Python) does not throttle short launches; --no-graph launches each step from Python
     graph = None
     if not args.no_graph:
         graph = torch.cuda.CUDAGraph()
@@ -120,8 +139,7 @@ def main():
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+    elapsed = time.perf_counter() - t0
     my_frames = float(sum(frames[i % P] for i in range(K)))
     if world > 1:
         t = torch.tensor([elapsed, my_frames, kern_ms], dtype=torch.float64, device=dev)
@@ -130,18 +148,29 @@ def main():
         tsum = t.clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         elapsed, total_frames, kern_ms = tmax[0].item(), tsum[1].item(), tmax[2].item()
-        # the exchange step before KNN (not part of the metric): all-gather of the 15-d vectors
-        from src.distributed import all_gather_rows
-        feat = fx(pool[0])["feat"]
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        g0 = time.perf_counter()
-        all_gather_rows(feat, total=C * world)
-        torch.cuda.synchronize(dev)
-        ag_ms = (time.perf_counter() - g0) * 1e3
     else:
         total_frames = my_frames
-        ag_ms = None
+    del graph
+
+    # the exchange step before KNN (not part of the metric): one packed all-gather of every
+    # per-clip result (76 B/clip)
+    ag = None
+    if world > 1:
+        out = fx(pool[0])
+        res = {k: out[k] for k in ("feat", "start_end", "n_frames", "status")}
+        gather_packed(res, args.clips)
+        torch.cuda.synchronize(dev)
+        ts = []
+        for _ in range(5):
+            dist.barrier()
+            g0 = time.perf_counter()
+            gather_packed(res, args.clips)
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - g0)
+        ag = {"ms": round(float(np.median(ts)) * 1e3, 4), "bytes": args.clips * OUT_BYTES_PER_CLIP,
+              "collectives": 1, "what": "feat/start_end/n_frames/status of all clips, packed, RCCL all_gather"}
+
+    sweep = window_sweep(args, fx, pool[0], dev, world, rank) if args.sweep_clips > 0 else None
     knn = knn_leg(args, dev, world) if args.knn_ref > 0 else None
 
     result = None
@@ -151,7 +180,8 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                 "kernel": "dsp::extract_kernel", "kernel_avg_ms": round(kern_ms, 5),
-                "algorithmic_bytes_per_launch": bytes_per_launch}
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "per_unit": "2*44100 B in + 76 B out per clip"}
         pmc = os.path.join(REPO, "profiles", "pmc_extract.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
@@ -169,36 +199,71 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / K * 1e3, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic (seeded 1 s int16 utterances: noise floor + fricative burst + voiced segment)",
-            "config": {"workload": "BASELINE configs[1]: %d x 1 s 44.1 kHz utterances per GPU, %s window, "
-                                   "E/M/ZCR + %s" % (C, args.window, "double-threshold VAD" if vad else "no VAD"),
-                       "clips_per_gpu": C, "samples_per_clip": N, "frame_length": L, "frame_shift": S,
-                       "window": args.window, "vad": vad, "input": "int16 PCM resident in HBM",
-                       "frames_per_step_per_gpu": round(my_frames / K, 1),
+            "data": "synthetic (seeded 1 s int16 utterances generated on the device: noise floor + "
+                    "fricative burst + voiced segment)",
+            "config": {"workload": "north star / BASELINE configs[3] batch: %d x 1 s 44.1 kHz utterances "
+                                   "sharded over %d GPU(s), %s window, E/M/ZCR + %s"
+                                   % (args.clips, world, args.window, "double-threshold VAD" if vad else "no VAD"),
+                       "clips": args.clips, "clips_per_gpu": C, "samples_per_clip": N, "frame_length": L,
+                       "frame_shift": S, "window": args.window, "vad": vad, "input": "int16 PCM resident in HBM",
+                       "frames_per_step": round(total_frames / K, 1),
                        "parallelism": "dp%d (clips sharded, no collective in the step)" % world,
-                       "launch": "hip graph of the %d steps" % K if graph is not None else "python loop"},
+                       "launch": "hip graph of the %d steps" % K if not args.no_graph else "python loop"},
             "roofline": roof,
         }
-        if ag_ms is not None:
-            result["allgather_feat_ms"] = round(ag_ms, 4)
+        if ag is not None:
+            result["allgather"] = ag
+        if sweep is not None:
+            result["window_sweep"] = sweep
         if knn is not None:
             result["knn"] = knn
         if world == 1 and not args.no_cpu:
-            result["cpu_baseline"] = cpu_baseline(host[0], L, S, args.window, vad, args.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(fx, pool[0], L, S, args.window, vad, args.cpu_seconds)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return result
 
 
+def window_sweep(args, fx0, batch, dev, world, rank):
+    """configs[2]: --sweep-clips clips (sharded over the ranks) x the three reference windows,
+    one fused launch per window over the resident PCM (experiment_window_comparison,
+    experiments/run_experiments.py:343-347).  Per-window frames/s from HIP-event launch times."""
+    import torch
+    import torch.distributed as dist
+    from src.distributed import shard_range
+    from src.pipeline import FeatureExtractor
+    lo, hi = shard_range(min(args.sweep_clips, args.clips), rank, world)
+    n = min(hi - lo, batch.shape[0])
+    sub = batch[:n]
+    stream = torch.cuda.current_stream(dev)
+    res = {}
+    for win in ("rectangular", "hamming", "hanning"):
+        fx = FeatureExtractor(fx0.L, fx0.S, win, fx0.do_vad, device=dev)
+        out = fx(sub)
+        assert not (out["status"].cpu().numpy() & 0xFF).any()
+        nv = ((sub.shape[1] - fx0.L) // fx0.S + 1) if fx0.do_vad else 0
+        fr = out["n_frames"].to(torch.int64).sum().item() + nv * n
+        ms = timed_launches(lambda: fx(sub), 5, stream)
+        t = torch.tensor([ms, fr], dtype=torch.float64, device=dev)
+        if world > 1:
+            tm = t.clone()
+            dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            ms, fr = tm[0].item(), t[1].item()
+        res[win] = {"frames_per_s": round(fr / (ms * 1e-3), 1), "kernel_ms": round(ms, 4)}
+    return {"config": "BASELINE configs[2]: %d x 1 s clips per window" % min(args.sweep_clips, args.clips),
+            "windows": res}
+
+
 def knn_leg(args, dev, world):
     """BASELINE configs[4] beside the headline metric: exact k-NN (KNeighborsClassifier
     semantics) of every one of --knn-ref synthetic z-scored 15-d vectors against all of them
-    (self excluded), queries sharded over the ranks, results gathered (RCCL all-gather).  Not
-    part of ``value``; reported as its own object with its VALU roofline (45 flop per pair)."""
+    (self excluded), queries sharded over the ranks, results gathered (one RCCL all-gather).
+    Not part of ``value``; reported as its own object with its VALU roofline (45 flop per pair)."""
     import torch
     import torch.distributed as dist
     from src.distributed import knn_sharded
@@ -218,7 +283,7 @@ def knn_leg(args, dev, world):
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        idx, dd, pred = knn_sharded(knn_classify, Xd, yd, Xd, args.knn_k, self_query=True)
+        knn_sharded(knn_classify, Xd, yd, Xd, args.knn_k, self_query=True)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -239,17 +304,35 @@ def knn_leg(args, dev, world):
             "data": "synthetic z-scored 15-d vectors around 10 class centres"}
 
 
-def cpu_baseline(batch, L, S, window, vad, budget_s):
+def host_cores():
+    """(cores this process may use, CPUs visible): the affinity set, capped by the cgroup CPU
+    quota when one is set (a GPU box shows the whole machine's CPUs but grants a share)."""
+    vis = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(math.ceil(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return (min(vis, quota) if quota else vis), vis, quota
+
+
+def cpu_baseline(fx, batch, L, S, window, vad, budget_s):
     """The C oracle (a restatement of the reference's numpy pipeline, oracle/) on the host
-    cores of this box, on a bounded sample of the same clips."""
+    cores of this box, on a bounded sample of the benchmark's own clips; its outputs on that
+    sample are compared with the GPU's (endpoints and frame counts exact, features 1e-5)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
     from src.pipeline import create_window
     w = create_window(window, L)
-    C, N = batch.shape
-    flat = np.ascontiguousarray(batch.reshape(-1))
+    n_host = min(batch.shape[0], 2000)
+    host = batch[:n_host].cpu().numpy()
+    C, N = host.shape
+    flat = np.ascontiguousarray(host.reshape(-1))
     off = np.arange(C + 1, dtype=np.int64) * N
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads, visible, quota = host_cores()
     nv = (N - L) // S + 1 if (vad and N >= L) else 0
 
     def run(nt, clips):
@@ -257,22 +340,31 @@ def cpu_baseline(batch, L, S, window, vad, budget_s):
         t = time.perf_counter()
         r = oracle.process_batch(flat[:o[-1]], o, L, S, w, do_vad=vad, nthreads=nt)
         dt = time.perf_counter() - t
-        return (nv * clips + int(r["n_frames"].sum())) / dt, dt
+        return (nv * clips + int(r["n_frames"].sum())) / dt, dt, r
 
     run(threads, min(C, 64 * threads))  # warm-up (thread arenas, page faults, clocks)
-    rate, dt = run(threads, C)
+    rate, dt, ref = run(threads, C)
+    # parity spot check of the sample against the device results of the same clips
+    got = {k: v[:C].cpu().numpy() for k, v in fx(batch[:C]).items()}
+    se_ok = bool(np.array_equal(got["start_end"], ref["start_end"]))
+    nf_ok = bool(np.array_equal(got["n_frames"], ref["n_frames"]))
+    rel = np.abs(got["feat"] - ref["feat"]) / np.maximum(np.abs(ref["feat"]), 1e-30)
     reps = 1
     total_frames, total_t = rate * dt, dt
     while total_t < budget_s and reps < 5000:
-        r2, d2 = run(threads, C)
+        r2, d2, _ = run(threads, C)
         total_frames += r2 * d2
         total_t += d2
         reps += 1
-    one, d1 = run(1, min(C, 200))
+    one, _, _ = run(1, min(C, 200))
     return {"value": round(total_frames / total_t, 1), "unit": "frames/s", "cores": threads, "kind": "port",
+            "host_cpus_visible": visible, "cgroup_cpu_quota": quota,
             "sample": "%d passes over %d of the benchmark's clips (%.1f s), C restatement of the reference "
-                      "numpy pipeline (oracle/dsp_oracle.c), %d threads; 1 thread: %.4g frames/s"
-                      % (reps, C, total_t, threads, one)}
+                      "numpy pipeline (oracle/dsp_oracle.c), %d threads (all usable cores: affinity %d, "
+                      "cgroup quota %s); 1 thread: %.4g frames/s"
+                      % (reps, C, total_t, threads, visible, quota, one),
+            "parity_on_sample": {"clips": C, "start_end_exact": se_ok, "n_frames_exact": nf_ok,
+                                 "feat_max_rel_err": float(np.nanmax(rel))}}
 
 
 if __name__ == "__main__":

@@ -30,27 +30,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "dsp_audiorec.h"
 #include "extract_layout.h"
 
-// implementation switches (A/B timing builds: tools/ab.sh)
-#ifndef DSP_P90PAR
-#define DSP_P90PAR 0  // p90: rank ranges over all waves (else: bitonic sort in wave 0; faster)
-#endif
-#ifndef DSP_R5SPLIT
-#define DSP_R5SPLIT 1  // R5: medians and moments on separate waves
-#endif
-#ifndef DSP_BUFLOAD
-#define DSP_BUFLOAD 1  // clip loads through a range-checked buffer descriptor
-#endif
-#ifndef DSP_ASM_ABS
-#define DSP_ASM_ABS 1  // R4: M += |y| as one VOP3 add with the abs modifier
-#endif
-#ifndef DSP_ASM_SQ2
-#define DSP_ASM_SQ2 1  // R1: k^2 pair sums as VOP3 v_dot2 with an inline zero
-#endif
-#ifndef DSP_NEAR0
-#define DSP_NEAR0 1  // R4: one packed subtraction of fl(mq) when |t0| <= 2
+#ifndef EXTRACT_R4_KV
+#define EXTRACT_R4_KV 9
 #endif
 
 namespace dsp {
@@ -67,10 +53,6 @@ static constexpr int NRV = 4 * RREG;       // 16-B vectors per thread in registe
     do {                                                                                         \
         if (threadIdx.x == 0 && p.stamps) p.stamps[(size_t)(clip) * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
-#define SKIP(bit) ((p.skip & (bit)) != 0)  // phase ablation for timing (outputs are garbage)
-// phase doubling (skip bits 8..): the phase runs twice; it is idempotent, so results and the
-// control flow after it are unchanged and the extra time / instructions are the phase's own
-#define REPS(bit) ((p.skip & ((bit) << 8)) ? 2 : 1)
 // per workgroup (row blockIdx.x, slots 16..): real-time and shader-clock stamps (WG_STAMP, at
 // entry and exit) and shader-clock stamps inside the prologue (WG_CK)
 #define WG_STAMP(k)                                                                          \
@@ -94,10 +76,11 @@ static constexpr int NRV = 4 * RREG;       // 16-B vectors per thread in registe
 #define STAMP(clip, k) \
     do {               \
     } while (0)
-#define SKIP(bit) false
-#define REPS(bit) 1
 #endif
 
+// The kernel's only argument.  clip_exact (out of line) reads it in place through the kernel's
+// kernarg-segment pointer: explicit arguments start at offset 0 of that segment, so the layout
+// must stay a plain aggregate passed by value as the FIRST and ONLY kernel parameter.
 struct ExtractParams {
     const int16_t *pcm;
     const int64_t *offsets;
@@ -113,10 +96,13 @@ struct ExtractParams {
     float *seq;
     int ld_seq;
     unsigned long long *stamps;  // diagnostic build only (else null)
-    int skip;                    // diagnostic build only: phases to skip (timing ablation)
     ExtractCarve cv;             // LDS layout, computed on the host (kernel arguments can be
                                  // re-read instead of being held in registers)
 };
+
+static_assert(__is_standard_layout(ExtractParams) && __is_trivially_copyable(ExtractParams),
+              "ExtractParams is read in place from the kernarg segment (clip_exact)");
+static_assert(sizeof(ExtractParams) <= 1024, "kernel argument block");
 
 typedef short short8 __attribute__((ext_vector_type(8)));
 template <bool B> struct BoolT {
@@ -364,8 +350,16 @@ __device__ __forceinline__ ClipRef clip_ref(const ExtractParams &p, int i)
     c.n = c.ok ? (int)nn : 0;
     c.base = o0 & ~(int64_t)7;
     c.lead = (int)(o0 - c.base);
-    c.nvec = (c.lead + c.n + 7) >> 3;
+    c.nvec = c.ok ? (c.lead + c.n + 7) >> 3 : 0;  // 0: loads of the clip read zeros
     c.nword = (c.lead + c.n + 31) >> 5;
+    return c;
+}
+__device__ __forceinline__ ClipRef clip_none()
+{
+    ClipRef c;
+    c.base = 0;
+    c.lead = c.n = c.nvec = c.nword = 0;
+    c.ok = false;
     return c;
 }
 
@@ -387,13 +381,12 @@ struct Ctx {
     int stamp_clip;  // clip index for the diagnostic stamps
 };
 
-// 16-B vectors of the clip buffer, read through a buffer descriptor spanning the clip's vectors
-// (DSP_BUFLOAD): a vector index past the clip reads zeros (hardware range check), so no address
+// 16-B vectors of the clip buffer, read through a buffer descriptor spanning the clip's vectors:
+// a vector index past the clip reads zeros (hardware range check), so no address
 // clamping, and the four vectors of a word share one offset register (immediate offsets).  The
 // clip's last vector may reach up to 15 bytes past offsets[B]; pcm is 16-B aligned, so such a
 // vector never crosses a page.  Bytes outside a clip are masked by every consumer ([lead, lead + n)
 // ranges, zero window weights), so no element-wise patching is needed.
-#if DSP_BUFLOAD
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t clip_rsrc(const ExtractParams &p, const ClipRef &c)
 {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<int16_t *>(p.pcm + c.base), 0, c.nvec * 16, 0x00020000);
@@ -409,42 +402,28 @@ __device__ __forceinline__ void issue_word(short8 *q, const ExtractParams &p, co
     for (int k = 0; k < 4; k++)
         q[k] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rs, 64 * w + 16 * k, 0, 0));
 }
-#else
-__device__ __forceinline__ short8 load_vec(const ExtractParams &p, const ClipRef &c, int v)
+
+// the clip's first RREG words into registers (word r * NT + tid -> regs[4r .. 4r+3])
+__device__ __forceinline__ void issue_clip(short8 (&regs)[NRV], const ExtractParams &p, const ClipRef &c)
 {
-    return reinterpret_cast<const short8 *>(p.pcm + c.base)[min(v, c.nvec - 1)];
-}
-// the four 16-B loads of word w (unconditional, clamped to the clip's last vector)
-__device__ __forceinline__ void issue_word(short8 *q, const ExtractParams &p, const ClipRef &c, int w)
-{
-    const short8 *src = reinterpret_cast<const short8 *>(p.pcm + c.base);
 #pragma unroll
-    for (int k = 0; k < 4; k++) q[k] = src[min(4 * w + k, c.nvec - 1)];
+    for (int r = 0; r < RREG; r++) issue_word(&regs[4 * r], p, c, r * NT + (int)threadIdx.x);
 }
-#endif
 
 // acc + |v| in one VOP3 add with the abs source modifier
 __device__ __forceinline__ float add_abs(float acc, float v)
 {
-#if DSP_ASM_ABS
     float r;
     asm("v_add_f32_e64 %0, |%1|, %2" : "=v"(r) : "v"(v), "v"(acc));
     return r;
-#else
-    return acc + fabsf(v);
-#endif
 }
 // k0^2 + k1^2 of a sample pair in one VOP3 v_dot2 with an inline-zero accumulator (the builtin
 // becomes v_mov 0 + v_dot2c)
 __device__ __forceinline__ int sq2(short2v d)
 {
-#if DSP_ASM_SQ2
     int r;
     asm("v_dot2_i32_i16 %0, %1, %1, 0" : "=v"(r) : "v"(d));
     return r;
-#else
-    return __builtin_amdgcn_sdot2(d, d, 0, false);
-#endif
 }
 
 __device__ __forceinline__ short2v half_pair(const short8 &x, int i)
@@ -851,6 +830,47 @@ __device__ __forceinline__ void ballot_select(Get get, int n, int r0, int r1, do
     }
 }
 
+// Endpoint frame ends (pass A): boundary t = 2f (start) / 2f + 1 (end) of VAD frame f lies inside
+// a buffer word that the frame only partly covers; returns that word (or -1: the boundary is
+// word aligned, or t >= 2 nv) and the covered element range [e0, e1) of it.
+__device__ __forceinline__ int vad_partial_word(const ClipRef &cur, int L, int S, int nv, int t, int &e0, int &e1)
+{
+    e0 = e1 = 0;
+    if (t >= 2 * nv) return -1;
+    const int f = t >> 1;
+    const bool end = t & 1;
+    const int u0 = cur.lead + f * S, u1 = u0 + L;
+    const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
+    if (!end && (u0 & 31)) {
+        e0 = u0 & 31;
+        e1 = min(32, u1 - 32 * wa);
+        return wa;
+    }
+    if (end && (u1 & 31) && (wb != wa || !(u0 & 31))) {
+        e0 = max(0, u0 - 32 * wb);
+        e1 = u1 & 31;
+        return wb;
+    }
+    return -1;
+}
+// exact moments (sum k, sum k^2) of elements [e0, e1) of one 32-sample word
+__device__ __forceinline__ void partial_moments(const short8 (&q)[4], int e0, int e1, int &t1, unsigned long long &t2)
+{
+#pragma unroll 1
+    for (int k = 0; k < 4; k++) {
+        const short8 v = k == 0 ? q[0] : k == 1 ? q[1] : k == 2 ? q[2] : q[3];
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            const int x = v[e];
+            const int ee = 8 * k + e;
+            if (ee >= e0 && ee < e1) {
+                t1 += x;
+                t2 += (unsigned)(x * x);
+            }
+        }
+    }
+}
+
 // One clip, start to finish; its first RREG words are already in flight into regs (word
 // r * NT + tid in regs[4r .. 4r+3]).  EXACT = false: endpoint energies from exact moments,
 // decisions certified; returns false on a near tie (the clip is then redone with EXACT = true
@@ -912,40 +932,29 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     // clips of up to RREG * NT words stream from the registers loaded before this call; longer
     // ones are read word by word here and again in R2 (the second read hits L2)
     const bool inreg = FAST || nword <= RREG * NT;
-    for (int rep_ = 0; rep_ < REPS(1); rep_++) {  // diagnostic doubling (REPS)
-        if (rep_) {
+    if (inreg) {
 #pragma unroll
-            for (int k = 0; k < NRV; k++) asm volatile("" : "+v"(regs[k]));  // no hoisting
-            K = 0;
-            kmin_s = 0x7fffffff;
-            kmax_s = -0x7fffffff - 1;
-            pmin = (short2v){32767, 32767};
-            pmax = (short2v){-32768, -32768};
+        for (int r = 0; r < RREG; r++) {
+            const int w = r * NT + tid;
+            if (w < nword) r1_word(&regs[4 * r], w);
         }
-        if (inreg) {
-#pragma unroll
-            for (int r = 0; r < RREG; r++) {
-                const int w = r * NT + tid;
-                if (w < nword && !SKIP(128)) r1_word(&regs[4 * r], w);
-            }
-        } else {
+    } else {
 #pragma unroll 1
-            for (int w = tid; w < nword; w += NT) {
-                short8 q[4];
-                issue_word(q, p, cur, w);
-                r1_word(q, w);
-            }
+        for (int w = tid; w < nword; w += NT) {
+            short8 q[4];
+            issue_word(q, p, cur, w);
+            r1_word(q, w);
         }
-        {
-            const int kmn = min(kmin_s, min((int)pmin.x, (int)pmin.y));
-            const int kmx = max(kmax_s, max((int)pmax.x, (int)pmax.y));
-            const long long ks = (long long)wave_sum(K);  // <= 64 threads' sums < 2^31
-            const int wmn = wave_min(kmn), wmx = wave_max(kmx);
-            if (lane == 0) {
-                sh->red_k[wid] = ks;
-                sh->red_a[wid] = wmn;
-                sh->red_b[wid] = wmx;
-            }
+    }
+    {
+        const int kmn = min(kmin_s, min((int)pmin.x, (int)pmin.y));
+        const int kmx = max(kmax_s, max((int)pmax.x, (int)pmax.y));
+        const long long ks = (long long)wave_sum(K);  // <= 64 threads' sums < 2^31
+        const int wmn = wave_min(kmn), wmx = wave_max(kmx);
+        if (lane == 0) {
+            sh->red_k[wid] = ks;
+            sh->red_a[wid] = wmn;
+            sh->red_b[wid] = wmx;
         }
     }
     __syncthreads();
@@ -994,26 +1003,36 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
         }
         c.posw[w] = P;
     };
-    for (int rep_ = 0; rep_ < REPS(2); rep_++) {  // diagnostic doubling (REPS)
-        if (rep_)
+    if (inreg) {
 #pragma unroll
-            for (int k = 0; k < NRV; k++) asm volatile("" : "+v"(regs[k]));  // no hoisting
-        if (inreg) {
-#pragma unroll
-            for (int r = 0; r < RREG; r++) {
-                const int w = r * NT + tid;
-                if (w < nword && !SKIP(64)) r2_word(&regs[4 * r], w);
-            }
-        } else {
+        for (int r = 0; r < RREG; r++) {
+            const int w = r * NT + tid;
+            if (w < nword) r2_word(&regs[4 * r], w);
+        }
+    } else {
 #pragma unroll 1
-            for (int w = tid; w < nword; w += NT) {
-                short8 q[4];
-                issue_word(q, p, cur, w);
-                r2_word(q, w);
-            }
+        for (int w = tid; w < nword; w += NT) {
+            short8 q[4];
+            issue_word(q, p, cur, w);
+            r2_word(q, w);
         }
     }
     if (tid < 2) c.posw[nword + tid] = 0;
+    // the partial words that endpoint pass A needs (FAST: one frame end per thread), issued
+    // before the barrier so that they are in flight while the workgroup synchronises
+    short8 qa[4];
+    int pa_w = -1, pa_e0 = 0, pa_e1 = 0;
+    if constexpr (!EXACT) {
+        if constexpr (FAST) {
+            const int pw = vad_partial_word(cur, L, S, nv, tid, pa_e0, pa_e1);
+            const __amdgpu_buffer_rsrc_t rs = clip_rsrc(p, cur);
+            const int off = pw >= 0 ? 64 * pw : 0x40000000;  // past the range: reads zeros
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                qa[k] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * k, 0, 0));
+            pa_w = pw;
+        }
+    }
     __syncthreads();
     STAMP(i, 2);
 
@@ -1022,47 +1041,32 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     if (nv > 0) {
         // frame f = buffer samples [u0, u0 + L): exact moments from the word sums plus the two
         // partial words at its ends, sign changes from the bits.
-        // Pass A, one thread per frame end: the partial word's moments (re-read from L2).
-        for (int rep_ = 0; rep_ < REPS(4); rep_++) {  // diagnostic doubling (REPS)
-            if (!EXACT && !SKIP(1)) {
-                for (int repa_ = 0; repa_ < REPS(128); repa_++)  // diagnostic doubling (REPS)
-                for (int t = tid; t < 2 * nv; t += NT) {
-                    const int f = t >> 1;
-                    const bool end = t & 1;
-                    const int u0 = lead + f * S, u1 = u0 + L;
-                    const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
-                    int pw = -1, e0 = 0, e1 = 0;
-                    if (!end && (u0 & 31)) {
-                        pw = wa;
-                        e0 = u0 & 31;
-                        e1 = min(32, u1 - 32 * wa);
-                    } else if (end && (u1 & 31) && (wb != wa || !(u0 & 31))) {
-                        pw = wb;
-                        e0 = max(0, u0 - 32 * wb);
-                        e1 = u1 & 31;
+        // Pass A, one thread per frame end: the partial word's moments (FAST: loaded before the
+        // next clip's prefetch; otherwise re-read from L2 here).
+        {
+            if constexpr (!EXACT) {
+                if constexpr (FAST) {
+                    if (tid < 2 * nv) {
+                        int t1 = 0;
+                        unsigned long long t2 = 0;
+                        if (pa_w >= 0) partial_moments(qa, pa_e0, pa_e1, t1, t2);
+                        c.pS1[tid] = t1;
+                        c.pS2[tid] = t2;
                     }
-                    int t1 = 0;
-                    unsigned long long t2 = 0;
-                    if (pw >= 0) {
-                        short8 q[4];
+                } else {
+                    for (int t = tid; t < 2 * nv; t += NT) {
+                        int e0, e1, t1 = 0;
+                        unsigned long long t2 = 0;
+                        const int pw = vad_partial_word(cur, L, S, nv, t, e0, e1);
+                        if (pw >= 0) {
+                            short8 q[4];
 #pragma unroll
-                        for (int k = 0; k < 4; k++) q[k] = load_vec(p, cur, 4 * pw + k);
-#pragma unroll 1
-                        for (int k = 0; k < 4; k++) {
-                            const short8 v = k == 0 ? q[0] : k == 1 ? q[1] : k == 2 ? q[2] : q[3];
-#pragma unroll
-                            for (int e = 0; e < 8; e++) {
-                                const int x = v[e];
-                                const int ee = 8 * k + e;
-                                if (ee >= e0 && ee < e1) {
-                                    t1 += x;
-                                    t2 += (unsigned)(x * x);
-                                }
-                            }
+                            for (int k = 0; k < 4; k++) q[k] = load_vec(p, cur, 4 * pw + k);
+                            partial_moments(q, e0, e1, t1, t2);
                         }
+                        c.pS1[t] = t1;
+                        c.pS2[t] = t2;
                     }
-                    c.pS1[t] = t1;
-                    c.pS2[t] = t2;
                 }
                 __syncthreads();
             }
@@ -1075,7 +1079,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                 int s1 = 0;  // |frame sum| <= L * 32768 < 2^31 for L < 65536
                 unsigned long long s2 = 0;
                 int zc = 0;
-                if (act && !SKIP(1)) {
+                if (act) {
                     const int u0 = lead + f * S, u1 = u0 + L;
                     if (!EXACT) {
                         const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
@@ -1109,8 +1113,8 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
             __syncthreads();
         }
         STAMP(i, 8);
-        for (int rep_ = 0; rep_ < REPS(8); rep_++) {  // diagnostic doubling (REPS)
-            // p90 order statistics (:198) by parallel ranks
+        {
+            // p90 order statistics (:198)
             {
                 const double vi = (double)(nv - 1) * 0.9;
                 int r0, r1;
@@ -1120,9 +1124,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                     r0 = (int)floor(vi);
                     r1 = r0 + 1;
                 }
-                if (SKIP(2)) {
-                    if (tid == 0) sh->pa = sh->pb = c.vE[r0];
-                } else if ((FAST || nv <= 128) && !DSP_P90PAR) {
+                if (FAST || nv <= 128) {
                     // wave 0: bitonic sort of the high halves of the order-preserving keys; the rank's
                     // element is the one holding that high half, or, when several do, the one of the
                     // right rank among them by the full key
@@ -1159,21 +1161,6 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                             sh->pb = pb;
                         }
                     }
-                } else if (nv <= 128) {
-                    // order-preserving keys in registers (lane + 64h); wave w takes candidates w,
-                    // w + 8, ...: #{keys below} and #{equal keys} by two ballots per half give the
-                    // ranks the candidate's value occupies (ties are equal values: no index needed)
-                    const unsigned long long k0 = lane < nv ? dkey(c.vE[lane]) : ~0ull;
-                    const unsigned long long k1 = lane + 64 < nv ? dkey(c.vE[lane + 64]) : ~0ull;
-                    for (int i2 = wid; i2 < nv; i2 += NWAVE) {
-                        const unsigned long long e = lane_read(i2 < 64 ? k0 : k1, i2 & 63);
-                        const int lt = __popcll(__ballot(k0 < e)) + __popcll(__ballot(k1 < e));
-                        const int eq = __popcll(__ballot(k0 == e)) + __popcll(__ballot(k1 == e));
-                        if (lane == 0) {
-                            if (r0 >= lt && r0 < lt + eq) sh->pa = dkey_value(e);
-                            if (r1 >= lt && r1 < lt + eq) sh->pb = dkey_value(e);
-                        }
-                    }
                 } else if (nv <= 256) {
                     ballot_select<double>([&](int j) { return c.vE[j]; }, nv, r0, r1, &sh->pa, &sh->pb, wid, lane);
                 } else {  // long clips: partial ranks over all waves
@@ -1190,20 +1177,11 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
             __syncthreads();
         }
         STAMP(i, 3);
-        for (int rep_ = 0; rep_ < REPS(16); rep_++) {  // diagnostic doubling (REPS)
-            if (SKIP(4)) {
-                if (tid == 0) {
-                    sh->n3 = 0;
-                    sh->n1 = min(30, nv - 1);
-                    sh->n6 = min(55, nv - 1);
-                    sh->exact = 0;
-                }
-            } else if (wid == 0) {
-                const int flag = vad_scan<!EXACT, FAST>(p, c, nv, lane);
-                if (lane == 0) sh->exact = (!EXACT && Mp > 0.0) ? flag : 0;
-            }
-            __syncthreads();
+        if (wid == 0) {
+            const int flag = vad_scan<!EXACT, FAST>(p, c, nv, lane);
+            if (lane == 0) sh->exact = (!EXACT && Mp > 0.0) ? flag : 0;
         }
+        __syncthreads();
         if (!EXACT && sh->exact) {  // near tie: redo in numpy's exact order after the loop
             return false;
         }
@@ -1265,10 +1243,10 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     // one 16-lane row per frame (4 frames per wave): lane rl of the row takes the frame's vectors
     // va + rl + 16k; every vector load of the frame is issued before any is used, and the row
     // sums need four DPP steps instead of a wave reduction
-    constexpr int R4_KV = 9;  // vectors per lane in one batch (frames up to 16*9*8-7 samples)
+    constexpr int R4_KV = EXTRACT_R4_KV;  // vectors per lane in one batch
     const int rl = lane & 15, row = lane >> 4;
-    for (int rep_ = 0; rep_ < REPS(32); rep_++) {  // diagnostic doubling (REPS)
-        for (int gi = wid; 4 * gi < (SKIP(8) ? 0 : F); gi += NWAVE) {
+    {
+        for (int gi = wid; 4 * gi < F; gi += NWAVE) {
             const int g = 4 * gi + row;
             const bool act = g < F;
             const int gc = act ? g : F - 1;
@@ -1294,7 +1272,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                 };
                 if (padded)
                     run(BoolT<true>(), BoolT<false>());
-                else if (DSP_NEAR0 && near0)
+                else if (near0)
                     run(BoolT<false>(), BoolT<true>());
                 else
                     run(BoolT<false>(), BoolT<false>());
@@ -1324,17 +1302,17 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     // ---- R5: 15-d statistics (compute_statistics x 3, fe.py:46-62) ------------------------
     // np.median: the middle order statistic (odd F) or the mean of the two middle ones
     const int r0 = (F - 1) / 2, r1 = F / 2;
-    for (int rep_ = 0; rep_ < REPS(64); rep_++) {  // diagnostic doubling (REPS)
+    {
         if (FAST || F <= 128) {
             // wave q alone handles sequence q (E, M, ZCR): lanes hold v[lane], v[lane + 64]; the
             // order statistics by ballot ranks over readlane'd candidates, then mean / std (fp64 sums)
             // and max / min -- no barrier
-            if (wid < (DSP_R5SPLIT ? 6 : 3) && !SKIP(48)) {
+            if (wid < 6) {
                 const int q = wid % 3;
                 auto get = [&](int j) -> float { return q == 0 ? c.fE[j] : q == 1 ? c.fM[j] : (float)c.fZ[j]; };
                 const bool in0 = lane < F, in1 = lane + 64 < F;
                 const float x0 = in0 ? get(lane) : 0.f, x1 = in1 ? get(lane + 64) : 0.f;
-                if (wid < 3 || !DSP_R5SPLIT) {  // median by an in-wave bitonic sort
+                if (wid < 3) {  // median by an in-wave bitonic sort
                     unsigned a[2] = {in0 ? fkey(x0) : ~0u, in1 ? fkey(x1) : ~0u};
                     float v0, v1;
                     if (F <= 64) {
@@ -1354,7 +1332,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                     }
                     if (lane == 0) featb[5 * q + 4] = (float)med;
                 }
-                if (wid >= 3 || !DSP_R5SPLIT) {  // mean, population std (fp64 sums), max, min
+                if (wid >= 3) {  // mean, population std (fp64 sums), max, min
                     const double s = wave_sum((in0 ? (double)x0 : 0.0) + (in1 ? (double)x1 : 0.0));
                     const float mx = wave_reduce(fmaxf(in0 ? x0 : -INFINITY, in1 ? x1 : -INFINITY), OpMax());
                     const float mn = wave_reduce(fminf(in0 ? x0 : INFINITY, in1 ? x1 : INFINITY), OpMin());
@@ -1442,11 +1420,6 @@ __device__ __forceinline__ void write_bad_clip(const ExtractParams &p, int i, in
     }
 }
 
-__device__ __forceinline__ void issue_clip(short8 (&regs)[NRV], const ExtractParams &p, const ClipRef &c)
-{
-#pragma unroll
-    for (int r = 0; r < RREG; r++) issue_word(&regs[4 * r], p, c, r * NT + (int)threadIdx.x);
-}
 
 __device__ __forceinline__ Ctx ctx_from(const ExtractCarve &cv, unsigned char *lds)
 {
@@ -1557,6 +1530,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     __syncthreads();
     WG_CK(20);
 
+    // clips blockIdx.x, blockIdx.x + G, ...  The host splits launches so that no workgroup walks
+    // more than EXTRACT_DEFER_CAP clips: the near-tie list below can never overflow.
     short8 regs[NRV];
     for (int i = blockIdx.x; i < p.B; i += G) {
         const ClipRef cur = clip_ref(p, i);
@@ -1567,13 +1542,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
         issue_clip(regs, p, cur);
         c.stamp_clip = i;
         const bool done = clip_body<false, FAST>(p, c, i, cur, regs);
-        if (!done && tid == 0) {
-            if (sh->ndefer < EXTRACT_DEFER_CAP) {
-                c.defer[sh->ndefer++] = i;
-            } else {  // list full (> EXTRACT_DEFER_CAP near ties in one workgroup)
-                p.status[i] = DSP_CLIP_UNCERTIFIED;
-            }
-        }
+        if (!done && tid == 0) c.defer[sh->ndefer++] = i;
         __syncthreads();  // LDS summaries are rewritten by the next clip
     }
     // near ties (rare): endpoint energies in numpy's exact float64 order
@@ -1590,16 +1559,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
 }  // namespace dsp
 
 static void *g_stamp_buffer = nullptr;
-static int g_skip = 0;
 #ifdef DSP_STAMPS
 extern "C" int dsp_debug_set_stamp_buffer(void *buf)
 {
     g_stamp_buffer = buf;
-    return 0;
-}
-extern "C" int dsp_debug_set_skip(int mask)
-{
-    g_skip = mask;
     return 0;
 }
 #endif
@@ -1612,7 +1575,8 @@ extern "C" size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int f
     return c.total <= EXTRACT_LDS_LIMIT ? (size_t)c.total : 0;
 }
 
-static int g_num_cus = 0;
+// CU count per device (the persistent grid), cached on first use of each device
+static int g_num_cus[64];
 
 extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, int B,
                                     int64_t max_len, int frame_length, int frame_shift,
@@ -1631,17 +1595,18 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     if (B == 0) return DSP_OK;
     const size_t lds = dsp_extract_lds_bytes(max_len, frame_length, frame_shift);
     if (lds == 0) return DSP_ERR_TOO_LONG;
-    if (g_num_cus == 0) {
-        int dev = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return DSP_ERR_HIP;
+    if (g_num_cus[dev] == 0) {
         hipDeviceProp_t prop;
-        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
-            return DSP_ERR_HIP;
-        g_num_cus = prop.multiProcessorCount;
+        if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return DSP_ERR_HIP;
+        g_num_cus[dev] = prop.multiProcessorCount;
         (void)hipFuncSetAttribute((const void *)dsp::extract_kernel<true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
         (void)hipFuncSetAttribute((const void *)dsp::extract_kernel<false>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
     }
+    const int num_cus = g_num_cus[dev];
     dsp::ExtractParams p;
     p.pcm = pcm;
     p.offsets = offsets;
@@ -1665,19 +1630,38 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     p.ld_seq = ld_seq;
     p.stamps = (unsigned long long *)g_stamp_buffer;
     p.cv = extract_carve((int)max_len, frame_length, frame_shift, EXTRACT_DEFER_CAP);
-    p.skip = g_skip;
     // persistent grid: two workgroups per CU when their LDS fits (one otherwise), each walking
     // clips blockIdx, blockIdx + grid, ...; the compile-time layout whenever the launch fits it
     const bool fast = extract_fast_fits((int)max_len, frame_length, frame_shift);
     const size_t lds_launch = fast ? (size_t)extract_carve_fast().total : lds;
     const int per_cu = lds_launch <= EXTRACT_LDS_SHARED ? 2 : 1;
-    const int slots = per_cu * g_num_cus;
-    const int grid = B < slots ? B : slots;
-    if (fast)
-        hipLaunchKernelGGL(dsp::extract_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch, (hipStream_t)stream, p);
-    else
-        hipLaunchKernelGGL(dsp::extract_kernel<false>, dim3(grid), dim3(dsp::NT), lds_launch, (hipStream_t)stream, p);
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? DSP_OK : DSP_ERR_HIP + (int)e;
+    const int slots = per_cu * num_cus;
+    // at most EXTRACT_DEFER_CAP clips per workgroup and launch, so every near tie fits the
+    // workgroup's redo list (larger batches: consecutive launches on the stream)
+    const int64_t chunk = (int64_t)slots * EXTRACT_DEFER_CAP;
+    for (int64_t b0 = 0; b0 < B; b0 += chunk) {
+        dsp::ExtractParams q = p;
+        const int nb = (int)std::min<int64_t>(chunk, B - b0);
+        q.B = nb;
+        q.offsets = offsets + b0;
+        q.feat = feat + 15 * b0;
+        q.start_end = start_end + 2 * b0;
+        q.n_frames = n_frames + b0;
+        q.status = status + b0;
+        if (vad_energy) {
+            q.vad_energy = vad_energy + b0 * ld_vad;
+            q.vad_zcr = vad_zcr + b0 * ld_vad;
+        }
+        if (seq) q.seq = seq + b0 * ld_seq * 3;
+        if (q.stamps) q.stamps = p.stamps + 32 * b0;
+        const int grid = nb < slots ? nb : slots;
+        if (fast)
+            hipLaunchKernelGGL(dsp::extract_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch, (hipStream_t)stream, q);
+        else
+            hipLaunchKernelGGL(dsp::extract_kernel<false>, dim3(grid), dim3(dsp::NT), lds_launch, (hipStream_t)stream, q);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return DSP_ERR_HIP + (int)e;
+    }
+    return DSP_OK;
 }
 

@@ -22,6 +22,7 @@ CLIP_EMPTY = 1
 CLIP_NO_AUDIO = 2
 CLIP_NO_FRAMES = 3
 CLIP_TOO_LONG = 4
+CLIP_UNCERTIFIED = 5  # reserved (never produced)
 CLIP_FLAG_VAD_EXACT = 0x100
 
 EXPORTS = ("dsp_extract_lds_bytes", "dsp_extract_features", "dsp_knn_workspace_bytes",

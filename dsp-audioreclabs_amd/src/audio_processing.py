@@ -131,6 +131,8 @@ _ERRORS = {
     _hip.CLIP_EMPTY: "zero-size array to reduction operation maximum which has no identity",
     _hip.CLIP_NO_AUDIO: "No audio remaining after preprocessing and endpoint detection.",
     _hip.CLIP_NO_FRAMES: "No frames provided for feature extraction.",
+    _hip.CLIP_TOO_LONG: "clip longer than the device pipeline supports",
+    _hip.CLIP_UNCERTIFIED: "endpoint decision could not be certified",
 }
 
 

@@ -2,9 +2,11 @@
 
 Clips are independent, so rank r of P processes the contiguous block ``shard_range(B, r, P)``
 with no collective inside the step.  The only exchange is before KNN: every rank needs the
-whole [B, 15] feature matrix (and labels), gathered with ``all_gather`` -- RCCL over xGMI
-with the "nccl" backend, gloo on CPU in the tests.  KNN then shards the queries and gathers
-the per-query results the same way.
+whole [B, 15] feature matrix (and the per-clip endpoints, frame counts, status), gathered with
+ONE ``all_gather`` of a packed byte matrix -- RCCL over xGMI with the "nccl" backend, gloo on
+CPU in the tests.  Block sizes follow from ``shard_range`` on every rank, so no size exchange
+and no host sync precede the collective.  KNN then shards the queries and gathers the per-query
+results (idx, dist, pred) the same way, again as one collective.
 """
 import torch
 import torch.distributed as dist
@@ -27,15 +29,62 @@ def shard_range(total, rank, world_size):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+def _pack_rows(tensors, rows):
+    """dict of tensors with ``rows`` leading rows -> (uint8 [rows, row_bytes], layout)."""
+    cols, layout = [], []
+    for name, t in tensors.items():
+        if t.shape[0] != rows:
+            raise ValueError("%s has %d rows, expected %d" % (name, t.shape[0], rows))
+        b = t.contiguous().reshape(rows, -1).view(torch.uint8)
+        layout.append((name, t.dtype, tuple(t.shape[1:]), b.shape[1]))
+        cols.append(b)
+    return torch.cat(cols, dim=1) if cols else None, layout
+
+
+def _unpack_rows(packed, layout):
+    out, c = {}, 0
+    n = packed.shape[0]
+    for name, dtype, tail, nb in layout:
+        out[name] = packed[:, c:c + nb].contiguous().view(dtype).reshape((n,) + tail)
+        c += nb
+    return out
+
+
+def gather_packed(tensors, total, group=None):
+    """All-gather several row-aligned tensors (this rank's ``shard_range`` block of ``total``
+    rows each) in rank order, as one collective over a packed byte matrix.
+
+    Returns {name: tensor [total, ...]} on every rank.
+    """
+    rank, ws = world()
+    if ws == 1:
+        return dict(tensors)
+    sizes = []
+    for r in range(ws):
+        lo, hi = shard_range(total, r, ws)
+        sizes.append(hi - lo)
+    rows = sizes[rank]
+    packed, layout = _pack_rows(tensors, rows)
+    m = max(sizes)
+    if rows < m:
+        packed = torch.cat([packed, packed.new_zeros((m - rows, packed.shape[1]))])
+    parts = [torch.empty_like(packed) for _ in range(ws)]
+    dist.all_gather(parts, packed, group=group)
+    full = torch.cat([p[:s] for p, s in zip(parts, sizes)])
+    return _unpack_rows(full, layout)
+
+
 def all_gather_rows(x, total=None, group=None):
     """Concatenate every rank's rows (in rank order) on every rank.
 
-    Blocks may differ in length by the shard_range rule; they are padded to the largest block
-    for the collective (all_gather needs equal shapes) and trimmed afterwards.
+    With ``total`` the blocks are the ``shard_range`` blocks (one collective); without it the
+    block sizes are exchanged first (blocks may be any size).
     """
     rank, ws = world()
     if ws == 1:
         return x
+    if total is not None:
+        return gather_packed({"x": x}, total, group)["x"]
     n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
     sizes = [torch.zeros_like(n) for _ in range(ws)]
     dist.all_gather(sizes, n, group=group)
@@ -46,33 +95,34 @@ def all_gather_rows(x, total=None, group=None):
         pad = torch.cat([x, x.new_zeros((m - x.shape[0],) + tuple(x.shape[1:]))])
     parts = [torch.empty_like(pad) for _ in range(ws)]
     dist.all_gather(parts, pad.contiguous(), group=group)
-    out = torch.cat([p[:s] for p, s in zip(parts, sizes)])
-    if total is not None and out.shape[0] != total:
-        raise RuntimeError("gathered %d rows, expected %d" % (out.shape[0], total))
-    return out
+    return torch.cat([p[:s] for p, s in zip(parts, sizes)])
 
 
 def extract_sharded(extract_fn, make_shard, total):
     """Run ``extract_fn(make_shard(lo, hi))`` on this rank's block and gather the results.
 
     ``extract_fn`` returns a dict of row-major tensors (feat, start_end, n_frames, status ...);
-    every entry is all-gathered so each rank ends with the full-batch dict.
+    all of them travel in one packed all-gather, so each rank ends with the full-batch dict.
     """
     rank, ws = world()
     lo, hi = shard_range(total, rank, ws)
     out = extract_fn(make_shard(lo, hi))
-    return {k: all_gather_rows(v, total) for k, v in out.items()}
+    return gather_packed(out, total)
 
 
 def knn_sharded(knn_fn, ref, labels, queries, k, self_query=False):
     """Query-sharded KNN: the reference set is replicated (post-gather), rank r answers the
-    queries of its shard_range block, and (idx, dist, pred) are gathered back.
+    queries of its shard_range block, and (idx, dist, pred) are gathered back in one collective.
 
     ``knn_fn(ref, labels, q, k, self_offset)`` -> (idx, dist, pred); with ``self_query`` the
     queries are the reference rows themselves and each excludes its own row.
     """
     rank, ws = world()
-    lo, hi = shard_range(queries.shape[0], rank, ws)
-    idx, d, pred = knn_fn(ref, labels, queries[lo:hi], k, lo if self_query else -1)
     n = queries.shape[0]
-    return all_gather_rows(idx, n), all_gather_rows(d, n), all_gather_rows(pred, n)
+    lo, hi = shard_range(n, rank, ws)
+    idx, d, pred = knn_fn(ref, labels, queries[lo:hi], k, lo if self_query else -1)
+    parts = {"idx": idx, "dist": d}
+    if pred is not None:
+        parts["pred"] = pred
+    g = gather_packed(parts, n)
+    return g["idx"], g["dist"], g.get("pred")

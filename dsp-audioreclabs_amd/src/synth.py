@@ -58,3 +58,44 @@ def make_batch(n_clips, base_seed=0, n_samples=SAMPLE_RATE, start=0, with_labels
     if with_labels:
         return out, labels
     return out
+
+
+def make_batch_device(n_clips, device, base_seed=0, n_samples=SAMPLE_RATE, start=0, chunk=2048):
+    """The same utterance recipe generated on the device (torch RNG, float32): for batches too
+    large to synthesise on the host (100 k clips = 8.8 GB).  Clips ``start .. start+n_clips-1``;
+    chunk ``c`` of ``chunk`` clips is drawn from a generator seeded with (base_seed, c), so a
+    shard that starts on a chunk boundary is reproducible on its own.  Returns int16
+    [n_clips, n_samples] on ``device``."""
+    import torch
+    out = torch.empty((n_clips, n_samples), dtype=torch.int16, device=device)
+    t = torch.arange(n_samples, device=device, dtype=torch.float32) / SAMPLE_RATE
+    idx = torch.arange(n_samples, device=device)
+    scale = min(1.0, n_samples / float(SAMPLE_RATE))
+    lo = 0
+    while lo < n_clips:
+        c = (start + lo) // chunk
+        hi = min(n_clips, (c + 1) * chunk - start)
+        m = hi - lo
+        g = torch.Generator(device=device)
+        g.manual_seed(int(base_seed) * 1000003 + c)
+        u = torch.rand((m, 9), generator=g, device=device)
+        f0 = 100.0 + 150.0 * u[:, 0:1]
+        dur = 0.3 + 0.2 * u[:, 1:2]
+        onset = 0.15 + 0.2 * u[:, 2:3]
+        amp = 0.2 + 0.4 * u[:, 3:4]
+        i0 = (onset * scale * SAMPLE_RATE).long()
+        i1 = torch.clamp(i0 + (dur * scale * SAMPLE_RATE).long(), max=n_samples)
+        x = torch.randn((m, n_samples), generator=g, device=device) * 0.003
+        seg = torch.zeros((m, n_samples), device=device)
+        for h in range(1, 6):
+            seg += torch.sin(2 * torch.pi * f0 * h * t + 2 * torch.pi * u[:, 3 + h:4 + h]) / h
+        inside = (idx >= i0) & (idx < i1)
+        seglen = (i1 - i0).clamp(min=2).float()
+        env = 0.5 - 0.5 * torch.cos(2 * torch.pi * (idx - i0).float() / (seglen - 1))
+        x += torch.where(inside, seg * env * amp / 1.5, 0.0)
+        b1 = torch.clamp(i0 - int(0.05 * scale * SAMPLE_RATE), min=0)
+        burst = (idx >= b1) & (idx < i0)
+        x += torch.where(burst, torch.randn((m, n_samples), generator=g, device=device) * 0.05, 0.0)
+        out[lo:hi] = torch.clamp(torch.round(x * 32767.0), -32768, 32767).to(torch.int16)
+        lo = hi
+    return out

@@ -42,8 +42,9 @@ extern "C" {
 #define DSP_CLIP_NO_AUDIO 2   /* "No audio remaining ..." (audio_processing.py:388-389) */
 #define DSP_CLIP_NO_FRAMES 3  /* "No frames provided ..." (feature_extraction.py:27-28) */
 #define DSP_CLIP_TOO_LONG 4   /* longer than the LDS capacity given at launch */
-#define DSP_CLIP_UNCERTIFIED 5 /* >512 near-tie endpoint decisions in one workgroup: not redone
-                                  (never observed; outputs of the clip are not written) */
+#define DSP_CLIP_UNCERTIFIED 5 /* reserved: an endpoint decision that could not be certified.
+                                  Never produced: launches are split so that every near tie
+                                  is redone on the exact path */
 /* status[b] flag bits (informational) */
 #define DSP_CLIP_FLAG_VAD_EXACT 0x100 /* endpoint decision was a near tie: re-decided on the
                                          bit-exact (numpy-order) fp64 path */

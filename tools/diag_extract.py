@@ -5,7 +5,7 @@ R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(R, "dsp-audioreclabs_amd"))
 import torch
 from src.pipeline import FeatureExtractor
-from src.synth import make_batch
+from src.synth import make_batch, make_batch_device
 
 def timeit(fx, x, reps=50):
     for _ in range(3): fx(x)
@@ -25,7 +25,7 @@ if STAMPS:
     stamp_buf = torch.zeros((C, 32), dtype=torch.int64, device="cuda")
     L_.dsp_debug_set_stamp_buffer.argtypes = [ctypes.c_void_p]
     assert L_.dsp_debug_set_stamp_buffer(ctypes.c_void_p(stamp_buf.data_ptr())) == 0
-x = torch.as_tensor(make_batch(C, base_seed=0)).cuda()
+x = torch.as_tensor(make_batch(C, base_seed=0)).cuda() if C <= 4000 else make_batch_device(C, "cuda")
 res = {}
 ONLY = os.environ.get("DIAG_VARIANTS")
 for name, kw in [("vad_hamming", dict(window_type="hamming", do_endpoint_detection=True)),
