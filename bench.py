@@ -56,7 +56,6 @@ def parse():
     ap.add_argument("--knn-ref", type=int, default=100000,
                     help="KNN leg (BASELINE configs[4]): reference rows, all of them queried (0: skip)")
     ap.add_argument("--knn-k", type=int, default=5)
-    ap.add_argument("--fused", action="store_true", help="one-kernel path (no workspace), for A/B")
     return ap.parse_args()
 
 
@@ -99,7 +98,7 @@ def main():
     # streams its input from HBM
     P = max(1, math.ceil(2 * LLC_BYTES / max(1, C * 2 * N)))
     pool = [make_batch_device(C, dev, base_seed=p, start=lo) for p in range(P)]
-    fx = FeatureExtractor(L, S, args.window, vad, device=dev, fused=args.fused)
+    fx = FeatureExtractor(L, S, args.window, vad, device=dev)
     stream = torch.cuda.current_stream(dev)
 
     # frames per batch (VAD frames + feature frames), counted from the kernel's own outputs

@@ -35,7 +35,6 @@
 #include "dsp_audiorec.h"
 #include "extract_layout.h"
 #include "dsp_device.h"
-#include "stream.h"
 
 #ifndef EXTRACT_R4_KV
 #define EXTRACT_R4_KV 9
@@ -1159,19 +1158,12 @@ extern "C" size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int f
 // CU count per device (the persistent grid), cached on first use of each device
 static int g_num_cus[64];
 
-extern "C" size_t dsp_extract_workspace_bytes(int64_t B, int64_t max_len, int frame_length, int frame_shift)
-{
-    if (B < 1 || !dsp_stream_fits(max_len, frame_length, frame_shift)) return 0;
-    return (size_t)B * (size_t)dsp_stream_layout(max_len, frame_length, frame_shift).stride;
-}
-
 extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, int B,
                                     int64_t max_len, int frame_length, int frame_shift,
                                     const double *window, int do_vad, double hi, double lo,
                                     double zr, float *feat, int32_t *start_end, int32_t *n_frames,
                                     int32_t *status, double *vad_energy, int32_t *vad_zcr,
-                                    int ld_vad, float *seq, int ld_seq, void *workspace,
-                                    size_t workspace_bytes, void *stream)
+                                    int ld_vad, float *seq, int ld_seq, void *stream)
 {
     if (B < 0 || !offsets || !window || !feat || !start_end || !n_frames || !status)
         return DSP_ERR_ARGS;
@@ -1195,13 +1187,6 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
     }
     const int num_cus = g_num_cus[dev];
-    // the two-kernel streaming path (stream.hip) whenever the clips fit its register plan and the
-    // caller supplied a workspace for at least one frame summary; the fused kernel otherwise
-    if (workspace && dsp_stream_fits(max_len, frame_length, frame_shift) &&
-        workspace_bytes >= (size_t)dsp_stream_layout(max_len, frame_length, frame_shift).stride)
-        return dsp_stream_launch(pcm, offsets, B, max_len, frame_length, frame_shift, window, do_vad, hi, lo,
-                                 zr, feat, start_end, n_frames, status, vad_energy, vad_zcr, ld_vad, seq,
-                                 ld_seq, workspace, workspace_bytes, num_cus, (hipStream_t)stream);
     dsp::ExtractParams p;
     p.pcm = pcm;
     p.offsets = offsets;

@@ -40,7 +40,7 @@ class FeatureExtractor:
 
     def __init__(self, frame_length, frame_shift, window_type="hamming", do_endpoint_detection=True,
                  energy_high_ratio=0.5, energy_low_ratio=0.1, zcr_threshold_ratio=1.5,
-                 return_vad_lists=False, return_sequences=False, device=None, fused=False):
+                 return_vad_lists=False, return_sequences=False, device=None):
         import torch
         self.device = device or _hip.require_device()
         self.L, self.S = int(frame_length), int(frame_shift)
@@ -52,27 +52,10 @@ class FeatureExtractor:
         self.ratios = (float(energy_high_ratio), float(energy_low_ratio), float(zcr_threshold_ratio))
         self.return_vad_lists = return_vad_lists
         self.return_sequences = return_sequences
-        self.fused = bool(fused)  # True: always the one-kernel path (no workspace)
         self._bufs = {}
-        self._ws = None
 
     def lds_bytes(self, max_len):
         return _hip.lib().dsp_extract_lds_bytes(int(max_len), self.L, self.S)
-
-    # frame summaries the workspace holds at most (larger batches run in consecutive chunks)
-    WORKSPACE_CLIPS = 65536
-
-    def _workspace(self, B, max_len):
-        """Device scratch for the two-kernel streaming path (None: the fused kernel runs)."""
-        import torch
-        if self.fused:
-            return None
-        need = _hip.lib().dsp_extract_workspace_bytes(min(B, self.WORKSPACE_CLIPS), int(max_len), self.L, self.S)
-        if need == 0:
-            return None
-        if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
-        return self._ws
 
     def _outputs(self, B, max_len):
         import torch
@@ -131,12 +114,11 @@ class FeatureExtractor:
         sq, lds_ = out.get("seq"), 0
         if sq is not None:
             lds_ = sq.shape[1]
-        ws = self._workspace(B, max_len)
         rc = _hip.lib().dsp_extract_features(
             _hip.ptr(pcm), _hip.ptr(off), B, max_len, self.L, self.S, _hip.ptr(self.window),
             int(self.do_vad), hi, lo, zr, _hip.ptr(out["feat"]), _hip.ptr(out["start_end"]),
             _hip.ptr(out["n_frames"]), _hip.ptr(out["status"]), _hip.ptr(ve), _hip.ptr(vz), ldv,
-            _hip.ptr(sq), lds_, _hip.ptr(ws), 0 if ws is None else ws.numel(), _hip.stream_handle(d))
+            _hip.ptr(sq), lds_, _hip.stream_handle(d))
         _hip.check(rc, "dsp_extract_features")
         return out
 

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define DSP_ABI_VERSION 2
+#define DSP_ABI_VERSION 1
 
 /* return codes */
 #define DSP_OK 0
@@ -53,15 +53,8 @@ extern "C" {
  * (0 if it exceeds the 160 KiB of one CU). Host-only helper. */
 size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int frame_shift);
 
-/* Bytes of device workspace that lets dsp_extract_features take the two-kernel streaming path
- * for B clips of up to max_len samples (one ~2 KB frame summary per clip; a smaller workspace is
- * used in consecutive chunks of whole summaries).  0 when that path does not apply (clips longer
- * than 49 145 samples, frame_length > 1276, frame_shift < 32, > 128 frames per clip).
- * Host-only helper. */
-size_t dsp_extract_workspace_bytes(int64_t B, int64_t max_len, int frame_length, int frame_shift);
-
 /*
- * dsp_extract_features -- the per-clip pipeline over a batch.
+ * dsp_extract_features -- fused per-clip pipeline, one workgroup per clip.
  * Replaces, per clip, the chain
  *   preprocess            src/audio_processing.py:78-90   (remove_dc :49-59, normalize_audio :62-75)
  *   endpoint_detection    src/audio_processing.py:135-275 (when do_vad != 0)
@@ -89,18 +82,12 @@ size_t dsp_extract_workspace_bytes(int64_t B, int64_t max_len, int frame_length,
  * seq       (optional, may be NULL): float32 [B, ld_seq, 3] per-frame (E, M, ZCR) -- the
  *           'sequence' method of extract_features_from_frames (:114-129); frames beyond
  *           ld_seq are dropped.
- * workspace (optional, may be NULL) device scratch of workspace_bytes.  With at least one frame
- *           summary (dsp_extract_workspace_bytes(1, ...)) and clips that fit, the batch runs as
- *           two kernels: an HBM-streaming pass that turns each clip into a frame summary, then
- *           one wave per clip for the endpoint decisions and statistics.  Otherwise one fused
- *           kernel, one workgroup per clip.  Results are identical.
  */
 int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, int B, int64_t max_len,
                          int frame_length, int frame_shift, const double *window, int do_vad,
                          double hi, double lo, double zr, float *feat, int32_t *start_end,
                          int32_t *n_frames, int32_t *status, double *vad_energy,
-                         int32_t *vad_zcr, int ld_vad, float *seq, int ld_seq, void *workspace,
-                         size_t workspace_bytes, void *stream);
+                         int32_t *vad_zcr, int ld_vad, float *seq, int ld_seq, void *stream);
 
 /*
  * KNN -- KNeighborsClassifier(n_neighbors=k) as configured in src/models.py:33-35 and used by

@@ -26,7 +26,7 @@ def lib():
 def test_header_declares_the_path():
     names = declared_functions()
     assert {"dsp_extract_features", "dsp_extract_lds_bytes", "dsp_knn_classify",
-            "dsp_knn_workspace_bytes", "dsp_extract_workspace_bytes", "dsp_zscore_fit", "dsp_zscore_apply", "dsp_abi_version"} <= set(names)
+            "dsp_knn_workspace_bytes", "dsp_zscore_fit", "dsp_zscore_apply", "dsp_abi_version"} <= set(names)
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -51,20 +51,6 @@ def test_lds_sizing(lib):
     assert lib.dsp_extract_lds_bytes(44100, 0, 441) == 0
 
 
-def test_extract_workspace_bytes(lib):
-    """The streaming path's workspace: one frame summary (< 4 KB) per clip when the clips fit its
-    register plan, 0 (fused kernel) otherwise."""
-    one = lib.dsp_extract_workspace_bytes(1, 44100, 1102, 441)
-    assert 0 < one <= 4096 and one % 128 == 0
-    assert lib.dsp_extract_workspace_bytes(1000, 44100, 1102, 441) == 1000 * one
-    assert lib.dsp_extract_workspace_bytes(10, 44100, 1024, 512) > 0
-    assert lib.dsp_extract_workspace_bytes(10, 49145, 1102, 441) > 0
-    assert lib.dsp_extract_workspace_bytes(10, 49146, 1102, 441) == 0   # past the register plan
-    assert lib.dsp_extract_workspace_bytes(10, 44100, 2205, 441) == 0   # window row too long
-    assert lib.dsp_extract_workspace_bytes(10, 44100, 882, 20) == 0     # shift < 32
-    assert lib.dsp_extract_workspace_bytes(0, 44100, 1102, 441) == 0
-
-
 def test_host_argument_checks(lib):
     """Argument errors are returned before anything touches the device."""
     from src import _hip
@@ -73,7 +59,7 @@ def test_host_argument_checks(lib):
     p = ctypes.cast(buf, ctypes.c_void_p)
     p2 = ctypes.c_void_p(p.value + 2)  # misaligned pcm
     args = lambda pcm, B, L=1102, S=441, feat=p: (pcm, p, B, 44100, L, S, p, 1, 0.5, 0.1, 1.5,
-                                                   feat, p, p, p, None, None, 0, None, 0, None, 0, None)
+                                                   feat, p, p, p, None, None, 0, None, 0, None)
     assert f(*args(p, -1)) == _hip.DSP_ERR_ARGS
     assert f(*args(p, 4, feat=None)) == _hip.DSP_ERR_ARGS
     assert f(*args(p2, 4)) == _hip.DSP_ERR_ARGS
