@@ -121,14 +121,16 @@ __device__ __forceinline__ double energy_from_moments(unsigned long long S2, lon
 
 // numpy float64 summation order (pairwise_sum in 8192-element buffered chunks): the certified
 // fallback of the endpoint energies.  Element i is x_i^2, x_i = fl(fl(k_i - mq) / M').
-__device__ __forceinline__ double xsq(const int16_t *clip, int i, double mq, double Mp)
+template <typename T>
+__device__ __forceinline__ double xsq(const T *clip, int64_t i, double mq, double Mp)
 {
     const double d = (double)clip[i] - mq;
     const double x = Mp > 0.0 ? d / Mp : d;
     return x * x;
 }
 
-__device__ __forceinline__ double pw_leaf(const int16_t *clip, int lo, int n, double mq, double Mp)
+template <typename T>
+__device__ __forceinline__ double pw_leaf(const T *clip, int64_t lo, int n, double mq, double Mp)
 {
     if (n < 8) {
         double res = 0.0;
@@ -146,9 +148,11 @@ __device__ __forceinline__ double pw_leaf(const int16_t *clip, int lo, int n, do
 }
 
 // iterative restatement of numpy's recursive pairwise_sum over [lo, lo+n), n <= 8192
-__device__ __forceinline__ double pw_block(const int16_t *clip, int lo, int n, double mq, double Mp)
+template <typename T>
+__device__ __forceinline__ double pw_block(const T *clip, int64_t lo, int n, double mq, double Mp)
 {
-    int s_lo[16], s_n[16], s_stage[16];
+    int64_t s_lo[16];
+    int s_n[16], s_stage[16];
     double s_left[16];
     int sp = 0;
     s_lo[0] = lo;
@@ -158,7 +162,8 @@ __device__ __forceinline__ double pw_block(const int16_t *clip, int lo, int n, d
     bool have = false;
     for (;;) {
         if (!have) {
-            const int cl = s_lo[sp], cn = s_n[sp];
+            const int64_t cl = s_lo[sp];
+            const int cn = s_n[sp];
             if (cn <= 128) {
                 ret = pw_leaf(clip, cl, cn, mq, Mp);
                 have = true;
@@ -175,7 +180,8 @@ __device__ __forceinline__ double pw_block(const int16_t *clip, int lo, int n, d
         }
         if (sp == 0) return ret;
         sp--;
-        const int pl = s_lo[sp], pn = s_n[sp];
+        const int64_t pl = s_lo[sp];
+        const int pn = s_n[sp];
         int n2 = pn / 2;
         n2 -= n2 % 8;
         if (s_stage[sp] == 1) {
@@ -192,7 +198,8 @@ __device__ __forceinline__ double pw_block(const int16_t *clip, int lo, int n, d
     }
 }
 
-__device__ __forceinline__ double np_energy_exact(const int16_t *clip, int lo, int n, double mq, double Mp)
+template <typename T>
+__device__ __forceinline__ double np_energy_exact(const T *clip, int64_t lo, int n, double mq, double Mp)
 {
     double total = 0.0;
     for (int c = 0; c < n; c += 8192) total += pw_block(clip, lo + c, min(8192, n - c), mq, Mp);

@@ -25,7 +25,8 @@ CLIP_TOO_LONG = 4
 CLIP_UNCERTIFIED = 5  # reserved (never produced)
 CLIP_FLAG_VAD_EXACT = 0x100
 
-EXPORTS = ("dsp_extract_lds_bytes", "dsp_extract_features", "dsp_knn_workspace_bytes",
+EXPORTS = ("dsp_extract_lds_bytes", "dsp_extract_features", "dsp_extract_general_workspace_bytes",
+           "dsp_extract_general", "dsp_knn_workspace_bytes",
            "dsp_knn_classify", "dsp_zscore_fit", "dsp_zscore_apply", "dsp_abi_version")
 
 _lib = None
@@ -57,6 +58,11 @@ def load_library(path=LIB_PATH):
     L.dsp_extract_features.restype = i32
     L.dsp_extract_features.argtypes = [vp, vp, i32, i64, i32, i32, vp, i32, dbl, dbl, dbl,
                                        vp, vp, vp, vp, vp, vp, i32, vp, i32, vp]
+    L.dsp_extract_general_workspace_bytes.restype = sz
+    L.dsp_extract_general_workspace_bytes.argtypes = [i64, i64, i32, i32]
+    L.dsp_extract_general.restype = i32
+    L.dsp_extract_general.argtypes = [vp, i32, vp, vp, i32, i64, i64, i32, i32, vp, i32, dbl, dbl, dbl,
+                                      vp, vp, vp, vp, vp, vp, i32, vp, i32, vp, sz, vp]
     L.dsp_knn_workspace_bytes.restype = sz
     L.dsp_knn_workspace_bytes.argtypes = [i64, i64, i32, i32]
     L.dsp_knn_classify.restype = i32

@@ -61,14 +61,15 @@ def load_wav(filepath):
 
 
 def load_wav_pcm(filepath):
-    """GPU-path form of load_wav: (int16 samples, sample_rate).
+    """GPU-path form of load_wav: (integer samples, sample_rate).
 
-    16-bit mono and 8-bit mono/stereo fit int16 exactly; 16-bit stereo (sums up to 17 bits)
-    raises ValueError for now."""
+    The samples are ``ints`` of decode_pcm_bytes (load_wav's audio up to a power-of-two scale,
+    which preprocess cancels): int16 for 16-bit mono and 8-bit mono/stereo; for 16-bit stereo the
+    channel sums, int16 when they fit and int32 otherwise (17 bits: dsp_extract_general)."""
     raw, sw, ch, sr = _read_wav(filepath)
     _, ints, _ = decode_pcm_bytes(raw, sw, ch)
     if ints.size and (ints.max() > 32767 or ints.min() < -32768):
-        raise ValueError("16-bit stereo needs the int32 sample path (not built yet)")
+        return ints.astype(np.int32), sr
     return ints.astype(np.int16), sr
 
 
@@ -157,10 +158,11 @@ def process_audio_file(filepath, frame_length, frame_shift,
 def process_pcm(pcm, sample_rate, frame_length, frame_shift, window_type='hamming',
                 do_endpoint_detection=True, energy_high_ratio=0.5, energy_low_ratio=0.1,
                 zcr_threshold_ratio=1.5):
-    """process_audio_file on int16 samples already in memory."""
+    """process_audio_file on integer samples already in memory (int16, or int32 for 16-bit
+    stereo channel sums)."""
     if window_type not in ("rectangular", "hamming", "hanning"):
         create_window(window_type, 1)  # raises the reference's ValueError
-    pcm = np.ascontiguousarray(pcm, dtype=np.int16)
+    pcm = np.ascontiguousarray(pcm, dtype=np.int32 if np.asarray(pcm).dtype == np.int32 else np.int16)
     n = pcm.size
     if n == 0:
         raise ValueError(_ERRORS[_hip.CLIP_EMPTY])

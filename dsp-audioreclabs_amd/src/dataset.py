@@ -47,12 +47,14 @@ def _decode(paths, n_threads):
 
 
 def pack_clips(clips):
-    """int16 clips -> (packed int16 [sum + 8], offsets int64 [B+1]); the 8-sample tail keeps the
-    last clip's 16-B vectors inside the buffer."""
+    """integer clips -> (packed [sum + 8], offsets int64 [B+1]); int16, or int32 when any clip
+    holds 16-bit stereo channel sums; the 8-sample tail keeps the last clip's 16-B vectors
+    inside the buffer."""
+    dt = np.int32 if any(c.dtype == np.int32 for c in clips) else np.int16
     lens = np.array([c.size for c in clips], dtype=np.int64)
     off = np.zeros(len(clips) + 1, dtype=np.int64)
     off[1:] = np.cumsum(lens)
-    return np.concatenate(list(clips) + [np.zeros(8, np.int16)]), off
+    return np.concatenate([c.astype(dt, copy=False) for c in clips] + [np.zeros(8, dt)]), off
 
 
 def _upload(pcm, off, device, stream=None):
@@ -78,9 +80,10 @@ def _threads(n_threads):
 class PCMDataset:
     """A directory of class sub-directories of WAV files, decoded once and resident in HBM.
 
-    Attributes: ``pcm`` int16 and ``offsets`` int64 device tensors (all readable clips back to
-    back), ``labels`` int array, ``files`` [(path, class)] of the kept clips, ``skipped``
-    [(path, reason)], ``class_names``.
+    Attributes: ``labels`` int array, ``files`` [(path, class)] of the kept clips, ``skipped``
+    [(path, reason)], ``class_names``; ``parts``: the device-resident PCM as (clip numbers,
+    packed pcm, int64 offsets, longest clip) groups -- int16 clips in one, and 16-bit stereo
+    clips whose channel sums need int32 in another (dsp_extract_general).
     """
 
     def __init__(self, data_dir, n_threads=None, device=None):
@@ -98,9 +101,36 @@ class PCMDataset:
         if not clips:
             raise ValueError("no readable WAV files under %s" % data_dir)
         self.labels = np.array([ci for _, ci in self.files], dtype=np.int64)
-        pcm, off = pack_clips(clips)
-        self.max_len = int(np.diff(off).max())
-        self.pcm, self.offsets, self._pinned = _upload(pcm, off, self.device)
+        self.parts, self._pinned = [], []
+        for wide in (False, True):
+            idx = np.array([j for j, c in enumerate(clips) if (c.dtype == np.int32) == wide], dtype=np.int64)
+            if idx.size == 0:
+                continue
+            pcm, off = pack_clips([clips[j] for j in idx])
+            dp, do, pin = _upload(pcm, off, self.device)
+            self.parts.append((idx, dp, do, int(np.diff(off).max())))
+            self._pinned.append(pin)
+        self.max_len = max(p_[3] for p_ in self.parts)
+
+    def _run(self, fx):
+        """Every part through ``fx`` -> per-clip host arrays in dataset order (per-frame arrays
+        zero-padded to the widest part)."""
+        n = len(self.files)
+        got = []
+        for idx, dp, do, ml in self.parts:
+            got.append((idx, {k: v.cpu().numpy() for k, v in fx(dp, do, max_len=ml).items()}))
+        res = {}
+        for k in got[0][1]:
+            width = max(o[k].shape[1] for _, o in got) if got[0][1][k].ndim > 1 else None
+            a0 = got[0][1][k]
+            shape = (n,) if width is None else (n, width) + a0.shape[2:]
+            res[k] = np.zeros(shape, dtype=a0.dtype)
+            for idx, o in got:
+                if width is None:
+                    res[k][idx] = o[k]
+                else:
+                    res[k][idx, :o[k].shape[1]] = o[k]
+        return res
 
     def __len__(self):
         return len(self.files)
@@ -113,9 +143,9 @@ class PCMDataset:
         are dropped, as the reference's loaders skip them (train_model.py:91-94)."""
         fx = FeatureExtractor(frame_length, frame_shift, window_type, do_endpoint_detection,
                               energy_high_ratio, energy_low_ratio, zcr_threshold_ratio, device=self.device)
-        out = fx(self.pcm, self.offsets, max_len=self.max_len)
-        feat = out["feat"].cpu().numpy().astype(np.float64)
-        ok = (out["status"].cpu().numpy() & 0xFF) == 0
+        out = self._run(fx)
+        feat = out["feat"].astype(np.float64)
+        ok = (out["status"] & 0xFF) == 0
         return feat[ok], self.labels[ok], ok
 
     def extract_both(self, frame_length, frame_shift, window_type='hamming', do_endpoint_detection=True,
@@ -132,15 +162,13 @@ class PCMDataset:
         fx = FeatureExtractor(frame_length, frame_shift, window_type, do_endpoint_detection,
                               energy_high_ratio, energy_low_ratio, zcr_threshold_ratio,
                               return_sequences=True, device=self.device)
-        out = fx(self.pcm, self.offsets, max_len=self.max_len)
-        ok = (out["status"].cpu().numpy() & 0xFF) == 0
-        import torch
-        torch_ok = torch.as_tensor(ok, device=out["seq"].device)
-        lengths = out["n_frames"].cpu().numpy().astype(np.int64)[ok]
+        out = self._run(fx)
+        ok = (out["status"] & 0xFF) == 0
+        lengths = out["n_frames"].astype(np.int64)[ok]
         width = int(lengths.max()) if lengths.size else 0
         cols = [0, 2] if use_only_energy_zcr else [0, 1, 2]
-        seq = out["seq"][torch_ok][:, :width][:, :, cols].to(torch.float64).cpu().numpy()
-        feat = out["feat"].cpu().numpy().astype(np.float64)[ok]
+        seq = out["seq"][ok][:, :width][:, :, cols].astype(np.float64)
+        feat = out["feat"].astype(np.float64)[ok]
         return feat, self.labels[ok], seq, lengths
 
     def sweep(self, configs, **kw):

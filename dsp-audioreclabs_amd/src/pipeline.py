@@ -76,16 +76,34 @@ class FeatureExtractor:
             self._bufs = {key: o}  # keep one shape alive
         return self._bufs[key]
 
-    def __call__(self, pcm, offsets=None, max_len=None):
-        """pcm: int16 [B, N] (uniform clips) or packed 1-D int16 with int64 offsets [B+1].
+    def fused_cap(self):
+        """Longest clip (samples) the fused kernel's on-chip plan holds at this (L, S)."""
+        if not hasattr(self, "_fcap"):
+            lib, lo, hi = _hip.lib(), 0, 1 << 24
+            while lo < hi:  # dsp_extract_lds_bytes is non-zero exactly for n <= cap
+                mid = (lo + hi + 1) // 2
+                if lib.dsp_extract_lds_bytes(mid, self.L, self.S) > 0:
+                    lo = mid
+                else:
+                    hi = mid - 1
+            self._fcap = lo
+        return self._fcap
 
-        Returns a dict of device tensors: feat [B,15] f32, start_end [B,2] i32,
-        n_frames [B] i32, status [B] i32 (+ vad_energy/vad_zcr, seq when requested).
-        The tensors are reused by the next call with the same shape.
+    def __call__(self, pcm, offsets=None, max_len=None):
+        """pcm: int16 or int32 [B, N] (uniform clips) or packed 1-D with int64 offsets [B+1].
+
+        int16 clips that fit the fused kernel's on-chip plan run in one fused launch; longer
+        clips, and int32 samples (16-bit stereo channel sums), run on dsp_extract_general in the
+        same stream order.  An explicit ``max_len`` caps the clips processed (longer ones report
+        DSP_CLIP_TOO_LONG).  Returns a dict of device tensors: feat [B,15] f32, start_end [B,2]
+        i32, n_frames [B] i32, status [B] i32 (+ vad_energy/vad_zcr, seq when requested).  The
+        tensors are reused by the next call with the same shape.
         """
         import torch
         d = self.device
-        pcm = _as_device(pcm, torch.int16, d)
+        wide = str(getattr(pcm, "dtype", "")) in ("int32", "torch.int32")
+        pcm = _as_device(pcm, torch.int32 if wide else torch.int16, d)
+        lens = None  # host clip lengths, when known without a device round trip
         if offsets is None:
             if pcm.dim() != 2:
                 raise ValueError("1-D packed pcm needs offsets")
@@ -94,16 +112,20 @@ class FeatureExtractor:
             if key not in self._bufs:
                 self._bufs[key] = torch.arange(B + 1, dtype=torch.int64, device=d) * N
             off = self._bufs[key]
-            max_len = N
+            true_max = N
+            lens = np.full(B, N, dtype=np.int64)
         else:
             if isinstance(offsets, np.ndarray) or not isinstance(offsets, torch.Tensor):
-                off_h = np.asarray(offsets, dtype=np.int64)
-                if max_len is None:
-                    max_len = int(np.max(np.diff(off_h))) if off_h.size > 1 else 1
-            elif max_len is None:
-                max_len = int(torch.max(offsets[1:] - offsets[:-1]).item())
+                lens = np.diff(np.asarray(offsets, dtype=np.int64))
+                true_max = int(lens.max()) if lens.size else 1
+            else:
+                true_max = None
             off = _as_device(offsets, torch.int64, d)
             B = off.numel() - 1
+            if true_max is None:
+                true_max = int(torch.max(off[1:] - off[:-1]).item()) if B > 0 else 1
+        if max_len is None:
+            max_len = true_max
         pcm = pcm.reshape(-1)
         max_len = max(int(max_len), 1)
         out = self._outputs(B, max_len)
@@ -114,12 +136,30 @@ class FeatureExtractor:
         sq, lds_ = out.get("seq"), 0
         if sq is not None:
             lds_ = sq.shape[1]
-        rc = _hip.lib().dsp_extract_features(
-            _hip.ptr(pcm), _hip.ptr(off), B, max_len, self.L, self.S, _hip.ptr(self.window),
-            int(self.do_vad), hi, lo, zr, _hip.ptr(out["feat"]), _hip.ptr(out["start_end"]),
-            _hip.ptr(out["n_frames"]), _hip.ptr(out["status"]), _hip.ptr(ve), _hip.ptr(vz), ldv,
-            _hip.ptr(sq), lds_, _hip.stream_handle(d))
-        _hip.check(rc, "dsp_extract_features")
+        args = (int(self.do_vad), hi, lo, zr, _hip.ptr(out["feat"]), _hip.ptr(out["start_end"]),
+                _hip.ptr(out["n_frames"]), _hip.ptr(out["status"]), _hip.ptr(ve), _hip.ptr(vz), ldv,
+                _hip.ptr(sq), lds_)
+        cap = 0 if wide else self.fused_cap()
+        if not wide and B > 0:
+            rc = _hip.lib().dsp_extract_features(
+                _hip.ptr(pcm), _hip.ptr(off), B, min(max_len, cap) if cap > 0 else max_len, self.L, self.S,
+                _hip.ptr(self.window), *args, _hip.stream_handle(d))
+            _hip.check(rc, "dsp_extract_features")
+        if B > 0 and (wide or max_len > cap):
+            # the clips the fused kernel cannot hold: one workgroup each, from global memory
+            if lens is None:
+                lens = (off[1:] - off[:-1]).cpu().numpy()
+            sel = np.nonzero((lens > cap) & (lens <= max_len) | (wide & (lens <= 0)))[0].astype(np.int32)
+            if sel.size:
+                idx = torch.as_tensor(sel).to(d)
+                nbytes = _hip.lib().dsp_extract_general_workspace_bytes(sel.size, max_len, self.L, self.S)
+                ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=d)
+                rc = _hip.lib().dsp_extract_general(
+                    _hip.ptr(pcm), 4 if wide else 2, _hip.ptr(off), _hip.ptr(idx), int(sel.size),
+                    0 if wide else cap, max_len, self.L, self.S, _hip.ptr(self.window), *args,
+                    _hip.ptr(ws), nbytes, _hip.stream_handle(d))
+                _hip.check(rc, "dsp_extract_general")
+                self._keep = (idx, ws)  # alive until the next call (stream-ordered use)
         return out
 
 

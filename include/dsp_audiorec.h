@@ -41,7 +41,8 @@ extern "C" {
 #define DSP_CLIP_EMPTY 1      /* zero-length clip: np.max of an empty array raises (audio_processing.py:72) */
 #define DSP_CLIP_NO_AUDIO 2   /* "No audio remaining ..." (audio_processing.py:388-389) */
 #define DSP_CLIP_NO_FRAMES 3  /* "No frames provided ..." (feature_extraction.py:27-28) */
-#define DSP_CLIP_TOO_LONG 4   /* longer than the LDS capacity given at launch */
+#define DSP_CLIP_TOO_LONG 4   /* longer than the max_len given at launch (dsp_extract_general
+                                 processes such clips) */
 #define DSP_CLIP_UNCERTIFIED 5 /* reserved: an endpoint decision that could not be certified.
                                   Never produced: launches are split so that every near tie
                                   is redone on the exact path */
@@ -88,6 +89,31 @@ int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, int B, int6
                          double hi, double lo, double zr, float *feat, int32_t *start_end,
                          int32_t *n_frames, int32_t *status, double *vad_energy,
                          int32_t *vad_zcr, int ld_vad, float *seq, int ld_seq, void *stream);
+
+/*
+ * dsp_extract_general -- the same pipeline for clips outside the fused kernel's on-chip plan:
+ * any length (process_audio_file has no limit, src/audio_processing.py:336-396) and samples
+ * wider than int16: 16-bit stereo, whose exact sample is the sum of the two channels (load_wav
+ * averages them, :35-44; the power-of-two scale cancels in preprocess).  One workgroup per clip
+ * from global memory; results identical to dsp_extract_features' where both apply.
+ *
+ * pcm          int16 (sample_bytes 2) or int32 (sample_bytes 4) samples, clips at offsets[b].
+ * clip_index   int32 [nclip] clip numbers b to process (device; NULL: b = 0 .. nclip-1).  Only
+ *              clips with min_len < len <= max_len are processed (min_len = 0: every clip,
+ *              empty ones reported DSP_CLIP_EMPTY); the outputs of the others are untouched, so
+ *              a batch can be split between the two entry points without a host round trip.
+ * outputs      as dsp_extract_features, indexed by clip number b.
+ * workspace    device scratch of dsp_extract_general_workspace_bytes(nclip, max_len, L, S).
+ */
+size_t dsp_extract_general_workspace_bytes(int64_t nclip, int64_t max_len, int frame_length,
+                                           int frame_shift);
+int dsp_extract_general(const void *pcm, int sample_bytes, const int64_t *offsets,
+                        const int32_t *clip_index, int nclip, int64_t min_len, int64_t max_len,
+                        int frame_length, int frame_shift, const double *window, int do_vad,
+                        double hi, double lo, double zr, float *feat, int32_t *start_end,
+                        int32_t *n_frames, int32_t *status, double *vad_energy, int32_t *vad_zcr,
+                        int ld_vad, float *seq, int ld_seq, void *workspace,
+                        size_t workspace_bytes, void *stream);
 
 /*
  * KNN -- KNeighborsClassifier(n_neighbors=k) as configured in src/models.py:33-35 and used by

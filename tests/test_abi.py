@@ -26,7 +26,7 @@ def lib():
 def test_header_declares_the_path():
     names = declared_functions()
     assert {"dsp_extract_features", "dsp_extract_lds_bytes", "dsp_knn_classify",
-            "dsp_knn_workspace_bytes", "dsp_zscore_fit", "dsp_zscore_apply", "dsp_abi_version"} <= set(names)
+            "dsp_knn_workspace_bytes", "dsp_extract_general", "dsp_extract_general_workspace_bytes", "dsp_zscore_fit", "dsp_zscore_apply", "dsp_abi_version"} <= set(names)
 
 
 def test_every_declared_symbol_is_exported(lib):
@@ -73,6 +73,15 @@ def test_host_argument_checks(lib):
     assert k(p, p, 100, p, 10, 15, 3, -1, 0, p, p, p, None, 0, None) == _hip.DSP_ERR_WORKSPACE
     assert k(p, p, 100, p, 0, 15, 3, -1, 0, None, None, None, None, 0, None) == _hip.DSP_OK
     assert lib.dsp_zscore_fit(None, 10, 15, p, p, None) == _hip.DSP_ERR_ARGS
+    g = lib.dsp_extract_general
+    gargs = lambda sb=2, ws=None, nws=0, n=4: (p, sb, p, None, n, 0, 44100, 1102, 441, p, 1, 0.5, 0.1, 1.5,
+                                              p, p, p, p, None, None, 0, None, 0, ws, nws, None)
+    assert g(*gargs(sb=3)) == _hip.DSP_ERR_ARGS
+    assert g(*gargs()) == _hip.DSP_ERR_WORKSPACE
+    assert g(*gargs(n=0)) == _hip.DSP_OK
+    one = lib.dsp_extract_general_workspace_bytes(1, 44100, 1102, 441)
+    assert one > 0 and lib.dsp_extract_general_workspace_bytes(3, 44100, 1102, 441) == 3 * one
+    assert lib.dsp_extract_general_workspace_bytes(1, 30 * 44100, 1102, 441) > 20 * one
     assert lib.dsp_zscore_apply(p, 0, 15, p, p, p, None) == _hip.DSP_OK
 
 
