@@ -22,7 +22,12 @@ from src.feature_extraction import normalize_features  # noqa: E402
 from src.models import create_classifier  # noqa: E402
 
 
-KNN_MAX_DIM = 32  # dsp_knn_classify's supported dimension range (include/dsp_audiorec.h)
+# the reference's classifier table (compare_feature_methods.py:147-151)
+CLASSIFIERS = {
+    'KNN': ('knn', {'n_neighbors': 3}),
+    'SVM': ('svm', {'C': 1.0, 'kernel': 'rbf'}),
+    'Decision Tree': ('decision_tree', {}),
+}
 
 
 def load_both_methods(data_dir=None, frame_length=None, frame_shift=None, window_type='hamming'):
@@ -34,32 +39,36 @@ def load_both_methods(data_dir=None, frame_length=None, frame_shift=None, window
     return X_stat, X_seq, y, lengths
 
 
-def compare(data_dir=None, classifiers=('knn', 'svm', 'decision_tree', 'naive_bayes'), test_size=0.2,
-            random_state=42):
-    """:124-214: the same classifiers on both feature sets -> {method: {classifier: accuracy}}."""
-    from sklearn.metrics import accuracy_score
+def compare(data_dir=None, classifiers=None, test_size=0.2, random_state=42):
+    """:124-214: each classifier on both feature sets, the reference's split and normalisation
+    -> {classifier: {'statistical': acc, 'sequence': acc, 'diff': sequence - statistical}}.
+    KNN on the flattened sequences (2 x max_frames columns) runs on the device like the 15-d
+    case (dsp_knn_classify's chunked high-dimensional screen + fp64 re-rank)."""
     from sklearn.model_selection import train_test_split
     X_stat, X_seq, y, _ = load_both_methods(data_dir)
+    X_flat = X_seq.reshape(len(X_seq), -1)
+    Xs_tr, Xs_te, y_tr, y_te = train_test_split(X_stat, y, test_size=test_size, random_state=random_state,
+                                                stratify=y)
+    Xq_tr, Xq_te, _, _ = train_test_split(X_flat, y, test_size=test_size, random_state=random_state, stratify=y)
+    Xs_tr, m, sd = normalize_features(Xs_tr)
+    Xs_te, _, _ = normalize_features(Xs_te, m, sd)
+    Xq_tr, m, sd = normalize_features(Xq_tr)
+    Xq_te, _, _ = normalize_features(Xq_te, m, sd)
     results = {}
-    for method, X in (("statistical", X_stat), ("sequence", X_seq.reshape(len(X_seq), -1))):
-        X_tr, X_te, y_tr, y_te = train_test_split(X, y, test_size=test_size, random_state=random_state,
-                                                  stratify=y)
-        X_tr, mean, std = normalize_features(X_tr)
-        X_te, _, _ = normalize_features(X_te, mean, std)
-        results[method] = {}
-        for name in classifiers:
-            if name == 'knn' and X.shape[1] > KNN_MAX_DIM:
-                # the fused KNN kernel (csrc/knn.hip) is built for the 15-d statistical vectors;
-                # the flattened sequences (2 x max_frames columns) are outside it -- reported, not
-                # silently computed elsewhere
-                results[method][name] = None
-                continue
-            clf = create_classifier(name)
-            clf.fit(X_tr, y_tr)
-            results[method][name] = float(accuracy_score(y_te, clf.predict(X_te)))
+    for name, (kind, params) in (classifiers or CLASSIFIERS).items():
+        acc = {}
+        for method, (tr, te) in (("statistical", (Xs_tr, Xs_te)), ("sequence", (Xq_tr, Xq_te))):
+            clf = create_classifier(kind, **params)
+            clf.fit(tr, y_tr)
+            acc[method] = float(clf.evaluate(te, y_te)['accuracy'])
+        results[name] = {'statistical': acc['statistical'], 'sequence': acc['sequence'],
+                         'diff': acc['sequence'] - acc['statistical']}
     return results
 
 
 if __name__ == "__main__":
-    for method, accs in compare().items():
-        print(method, {k: (None if v is None else round(v, 4)) for k, v in accs.items()})
+    res = compare()
+    for name, r in res.items():
+        print("%-15s statistical %.4f  sequence %.4f  diff %+.4f" % (name, r['statistical'], r['sequence'], r['diff']))
+    print("mean  statistical %.4f  sequence %.4f" % (np.mean([r['statistical'] for r in res.values()]),
+                                                      np.mean([r['sequence'] for r in res.values()])))

@@ -173,6 +173,85 @@ __global__ __launch_bounds__(KNN_TQ) void knn_screen(const float *__restrict__ r
         }
 }
 
+// High-dimensional rows (D > 32: the sequence method's flattened (E, ZCR) sequences,
+// compare_feature_methods.py:117-154): direct form sum (q - r)^2 in fp32, the dimensions walked
+// in chunks of 16 against LDS tiles of 64 reference rows; one query per thread, 64 running
+// distances in registers, then the same top-KC insertion.
+static constexpr int HD_ROWS = 64, HD_COLS = 16;
+template <int KC>
+__global__ __launch_bounds__(KNN_TQ) void knn_screen_hd(const float *__restrict__ ref32, int64_t Nr,
+                                                         const float *__restrict__ q32, int64_t Nq, int DP,
+                                                         int64_t self_offset, int nsplit,
+                                                         float *__restrict__ cand_d, int *__restrict__ cand_i)
+{
+    __shared__ __attribute__((aligned(16))) float tile[HD_ROWS * HD_COLS];
+    const int tid = threadIdx.x;
+    const int64_t q = (int64_t)blockIdx.x * KNN_TQ + tid;
+    const int sp = blockIdx.y;
+    const int64_t per = (Nr + nsplit - 1) / nsplit;
+    const int64_t r0 = (int64_t)sp * per, r1 = min(Nr, r0 + per);
+    const int64_t self = (self_offset >= 0 && q < Nq) ? self_offset + q : -1;
+    const float *qrow = q32 + (q < Nq ? q : 0) * DP;
+    float dl[KC];
+    int il[KC];
+#pragma unroll
+    for (int i = 0; i < KC; i++) {
+        dl[i] = INFINITY;
+        il[i] = -1;
+    }
+    for (int64_t t0 = r0; t0 < r1; t0 += HD_ROWS) {
+        const int nt = (int)min((int64_t)HD_ROWS, r1 - t0);
+        float d[HD_ROWS];
+#pragma unroll
+        for (int u = 0; u < HD_ROWS; u++) d[u] = 0.f;
+        for (int c0 = 0; c0 < DP; c0 += HD_COLS) {
+            float qc[HD_COLS];
+#pragma unroll
+            for (int c4 = 0; c4 < HD_COLS / 4; c4++) {
+                const float4 v = reinterpret_cast<const float4 *>(qrow + c0)[c4];
+                qc[4 * c4] = v.x;
+                qc[4 * c4 + 1] = v.y;
+                qc[4 * c4 + 2] = v.z;
+                qc[4 * c4 + 3] = v.w;
+            }
+            __syncthreads();
+            {  // 64 rows x 16 columns, one float4 per thread
+                const int row = tid >> 2, c4 = tid & 3;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (row < nt) v = reinterpret_cast<const float4 *>(ref32 + (t0 + row) * DP + c0)[c4];
+                reinterpret_cast<float4 *>(tile)[tid] = v;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < HD_ROWS; u++) {
+                const float4 *rv = reinterpret_cast<const float4 *>(tile + u * HD_COLS);
+#pragma unroll
+                for (int c4 = 0; c4 < HD_COLS / 4; c4++) {
+                    const float4 r = rv[c4];
+                    float t;
+                    t = qc[4 * c4 + 0] - r.x; d[u] = fmaf(t, t, d[u]);
+                    t = qc[4 * c4 + 1] - r.y; d[u] = fmaf(t, t, d[u]);
+                    t = qc[4 * c4 + 2] - r.z; d[u] = fmaf(t, t, d[u]);
+                    t = qc[4 * c4 + 3] - r.w; d[u] = fmaf(t, t, d[u]);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < HD_ROWS; u++) {
+            const int64_t r = t0 + u;
+            if (u < nt && r != self) topk_insert<KC>(dl, il, d[u], (int)r);
+        }
+    }
+    if (q < Nq) {
+        const size_t o = ((size_t)sp * Nq + q) * KC;
+#pragma unroll
+        for (int i = 0; i < KC; i++) {
+            cand_d[o + i] = dl[i];
+            cand_i[o + i] = il[i];
+        }
+    }
+}
+
 #pragma clang fp contract(off)
 // sklearn euclidean_rdist: sequential d += t*t, no FMA
 __device__ __forceinline__ double rdist64(const double *__restrict__ a, const double *__restrict__ b, int D)
@@ -236,9 +315,10 @@ template <int KC>
 __global__ void knn_merge(const double *__restrict__ ref, const double *__restrict__ query,
                           int64_t Nr, int64_t Nq, int D, int k, int nsplit, int64_t self_offset,
                           const float *__restrict__ cand_d, const int *__restrict__ cand_i,
-                          const unsigned int *maxnorm_bits, const int32_t *__restrict__ labels,
-                          int32_t *__restrict__ idx, double *__restrict__ dist,
-                          int32_t *__restrict__ pred, int *fb_count, int *fb_list)
+                          const unsigned int *maxnorm_bits, double err_rel, double err_abs,
+                          const int32_t *__restrict__ labels, int32_t *__restrict__ idx,
+                          double *__restrict__ dist, int32_t *__restrict__ pred, int *fb_count,
+                          int *fb_list)
 {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= Nq) return;
@@ -253,10 +333,9 @@ __global__ void knn_merge(const double *__restrict__ ref, const double *__restri
     double qn = 0.0;
     for (int c = 0; c < D; c++) qn += qx[c] * qx[c];
     // |fp32 screened distance - fp64 distance| <= err(d): fp32 rounding of the inputs and of the
-    // sum (direct or expanded form)
+    // sum (direct or expanded form), coefficients from the host (knn_err_coeffs)
     const double rmax = (double)__uint_as_float(*maxnorm_bits);
-    // (expanded form: 16 FMA roundings of partial sums bounded by 2 (|q|^2 + |r|^2))
-    auto err = [&](double d) { return 2e-6 * d + 4e-6 * (qn + rmax) + 1e-30; };
+    auto err = [&](double d) { return err_rel * d + err_abs * (qn + rmax) + 1e-30; };
     // pass 1 (fp32 only): the k-th smallest screened distance t32 and the screening cut-off of
     // every split whose candidate list is full
     float k32[KMAX];
@@ -409,7 +488,10 @@ struct KnnLayout {
     size_t ref32, q32, cand_d, cand_i, misc, total;
     int DP, KC, nsplit;
     bool exp;  // expanded-form screening (a spare padded column holds |r|^2)
+    bool hd;   // D > 32: chunked direct-form screen (knn_screen_hd)
 };
+
+static constexpr int KNN_DMAX = 4096;
 
 int pick_kc(int k)
 {
@@ -420,9 +502,9 @@ int pick_kc(int k)
     return 36;
 }
 
-int pick_nsplit(int64_t Nr, int64_t Nq)
+int pick_nsplit(int64_t Nr, int64_t Nq, int qpb)
 {
-    const int64_t qblocks = (Nq + dsp::KNN_TQ * dsp::KNN_QP - 1) / (dsp::KNN_TQ * dsp::KNN_QP);
+    const int64_t qblocks = (Nq + qpb - 1) / qpb;
     // Enough workgroups to fill the chip (two per CU), as few reference splits as that allows:
     // a longer split makes a screened distance that enters its top list rarer (~KC / rows seen),
     // and a wave pays for an insertion whenever any of its 64 lanes makes one
@@ -443,10 +525,11 @@ size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
 {
     KnnLayout l;
-    l.DP = D <= 16 ? 16 : 32;
-    l.exp = D < l.DP;
+    l.hd = D > 32;
+    l.DP = D <= 16 ? 16 : D <= 32 ? 32 : (D + 15) & ~15;
+    l.exp = !l.hd && D < l.DP;
     l.KC = pick_kc(k);
-    l.nsplit = pick_nsplit(Nr, Nq);
+    l.nsplit = pick_nsplit(Nr, Nq, l.hd ? dsp::KNN_TQ : dsp::KNN_TQ * dsp::KNN_QP);
     size_t o = 0;
     l.ref32 = o; o += al((size_t)Nr * l.DP * 4);
     l.q32 = o;   o += al((size_t)Nq * l.DP * 4);
@@ -472,17 +555,34 @@ void launch_screen(dim3 g, hipStream_t s, bool exp, const float *r, int64_t Nr, 
 template <int KC>
 void launch_merge(dim3 g, dim3 b, hipStream_t s, const double *ref, const double *query,
                   int64_t Nr, int64_t Nq, int D, int k, int nsplit, int64_t self, const float *cd,
-                  const int *ci, const unsigned *mx, const int32_t *lbl, int32_t *idx, double *dist,
-                  int32_t *pred, int *fbc, int *fbl)
+                  const int *ci, const unsigned *mx, double er, double ea, const int32_t *lbl,
+                  int32_t *idx, double *dist, int32_t *pred, int *fbc, int *fbl)
 {
     hipLaunchKernelGGL((dsp::knn_merge<KC>), g, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self,
-                       cd, ci, mx, lbl, idx, dist, pred, fbc, fbl);
+                       cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl);
+}
+
+// err(d) = er * d + ea * (|q|^2 + max |r|^2) bounds |fp32 screened - fp64| distance.
+//  * D <= 32, expanded form |q|^2 + q'.r' (or direct form at D = 16 / 32): <= 16 FMA roundings of
+//    partial sums bounded by 2 (|q|^2 + |r|^2), plus the fp32 rounding of the inputs;
+//  * D > 32, direct form: D sequential FMAs of non-negative terms, each (q - r) rounded once:
+//    relative (D + 3) u on the sum, plus 4 u (|q|^2 + |r|^2) from the inputs (u = 2^-24); 2x margin.
+void knn_err_coeffs(const KnnLayout &l, int D, double &er, double &ea)
+{
+    if (!l.hd) {
+        er = 2e-6;
+        ea = 4e-6;
+    } else {
+        const double u = 1.0 / 16777216.0;
+        er = 2.0 * (D + 3) * u * 1.05;
+        ea = 2.0 * 4.2 * u;
+    }
 }
 }  // namespace
 
 extern "C" size_t dsp_knn_workspace_bytes(int64_t Nr, int64_t Nq, int D, int k)
 {
-    if (Nr < 0 || Nq < 0 || D < 1 || D > 32 || k < 1 || k > 32) return 0;
+    if (Nr < 0 || Nq < 0 || D < 1 || D > KNN_DMAX || k < 1 || k > 32) return 0;
     return knn_layout(Nr, Nq, D, k).total;
 }
 
@@ -491,7 +591,7 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
                                 int n_classes, int32_t *idx, double *dist, int32_t *pred,
                                 void *workspace, size_t workspace_bytes, void *stream)
 {
-    if (D < 1 || D > 32 || k < 1 || k > dsp::KMAX || Nr < 0 || Nq < 0) return DSP_ERR_ARGS;
+    if (D < 1 || D > KNN_DMAX || k < 1 || k > dsp::KMAX || Nr < 0 || Nq < 0) return DSP_ERR_ARGS;
     if (Nr > 0x7fffffff || (Nq > 0 && (!query || !idx || !dist)) || (Nr > 0 && !ref))
         return DSP_ERR_ARGS;
     if (Nq == 0) return DSP_OK;
@@ -514,20 +614,35 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
                            ref, Nr, D, l.DP, l.exp ? 1 : 0, ref32, mx);
     hipLaunchKernelGGL(dsp::knn_convert, dim3((unsigned)((Nq + cb - 1) / cb)), dim3(cb), 0, s,
                        query, Nq, D, l.DP, l.exp ? 2 : 0, q32, (unsigned *)nullptr);
-    const dim3 g((unsigned)((Nq + dsp::KNN_TQ * dsp::KNN_QP - 1) / (dsp::KNN_TQ * dsp::KNN_QP)), (unsigned)l.nsplit);
+    if (l.hd) {
+        const dim3 g((unsigned)((Nq + dsp::KNN_TQ - 1) / dsp::KNN_TQ), (unsigned)l.nsplit);
+        switch (l.KC) {
+#define DSP_SCREEN_HD(KCV)                                                                        \
+    case KCV:                                                                                     \
+        hipLaunchKernelGGL((dsp::knn_screen_hd<KCV>), g, dim3(dsp::KNN_TQ), 0, s, ref32, Nr, q32, Nq, \
+                           l.DP, self_offset, l.nsplit, cd, ci);                                  \
+        break
+            DSP_SCREEN_HD(8); DSP_SCREEN_HD(16); DSP_SCREEN_HD(24); DSP_SCREEN_HD(36);
+#undef DSP_SCREEN_HD
+        }
+    } else {
+        const dim3 g((unsigned)((Nq + dsp::KNN_TQ * dsp::KNN_QP - 1) / (dsp::KNN_TQ * dsp::KNN_QP)), (unsigned)l.nsplit);
 #define DSP_SCREEN(DPV, KCV)                                                                  \
     if (l.DP == DPV && l.KC == KCV) launch_screen<DPV, KCV>(g, s, l.exp, ref32, Nr, q32, Nq, self_offset, \
                                                             l.nsplit, cd, ci)
-    DSP_SCREEN(16, 8); DSP_SCREEN(16, 16); DSP_SCREEN(16, 24); DSP_SCREEN(16, 36);
-    DSP_SCREEN(32, 8); DSP_SCREEN(32, 16); DSP_SCREEN(32, 24); DSP_SCREEN(32, 36);
+        DSP_SCREEN(16, 8); DSP_SCREEN(16, 16); DSP_SCREEN(16, 24); DSP_SCREEN(16, 36);
+        DSP_SCREEN(32, 8); DSP_SCREEN(32, 16); DSP_SCREEN(32, 24); DSP_SCREEN(32, 36);
 #undef DSP_SCREEN
+    }
+    double er, ea;
+    knn_err_coeffs(l, D, er, ea);
     const int32_t *lbl = pred ? ref_labels : nullptr;
     const dim3 mg((unsigned)((Nq + 127) / 128)), mb(128);
     switch (l.KC) {
-    case 8: launch_merge<8>(mg, mb, s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, lbl, idx, dist, pred, fbc, fbl); break;
-    case 16: launch_merge<16>(mg, mb, s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, lbl, idx, dist, pred, fbc, fbl); break;
-    case 24: launch_merge<24>(mg, mb, s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, lbl, idx, dist, pred, fbc, fbl); break;
-    default: launch_merge<36>(mg, mb, s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, lbl, idx, dist, pred, fbc, fbl); break;
+    case 8: launch_merge<8>(mg, mb, s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
+    case 16: launch_merge<16>(mg, mb, s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
+    case 24: launch_merge<24>(mg, mb, s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
+    default: launch_merge<36>(mg, mb, s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
     }
     const unsigned fbgrid = (unsigned)(Nq < 512 ? Nq : 512);
     hipLaunchKernelGGL(dsp::knn_fallback, dim3(fbgrid), dim3(dsp::FB_T), 0, s, ref, query, Nr, D,

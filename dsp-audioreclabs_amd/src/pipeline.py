@@ -191,7 +191,7 @@ def knn_classify(ref, ref_labels, query, k, self_offset=-1, n_classes=None, with
         n_classes = 0
     ws_bytes = _hip.lib().dsp_knn_workspace_bytes(Nr, Nq, D, k)
     if ws_bytes == 0 and Nq > 0:
-        raise ValueError("unsupported KNN shape (1 <= D <= 32, 1 <= k <= 32)")
+        raise ValueError("unsupported KNN shape (1 <= D <= 4096, 1 <= k <= 32)")
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=d)
     idx = torch.empty((Nq, k), dtype=torch.int32, device=d)
     dist = torch.empty((Nq, k), dtype=torch.float64, device=d)

@@ -132,7 +132,8 @@ int dsp_extract_general(const void *pcm, int sample_bytes, const int64_t *offset
  * idx        int32 [Nq, k] (-1 where fewer than k candidates), dist float64 [Nq, k],
  * pred       int32 [Nq] (may be NULL, or ref_labels NULL, to skip the vote)
  * workspace  device scratch of dsp_knn_workspace_bytes(Nr, Nq, D, k) bytes.
- * Requires 1 <= D <= 32, 1 <= k <= 32.
+ * Requires 1 <= D <= 4096, 1 <= k <= 32.  D <= 32: queries in registers, reference tiles in LDS;
+ * D > 32 (the sequence method's flattened features): dimensions walked in chunks of 16.
  */
 size_t dsp_knn_workspace_bytes(int64_t Nr, int64_t Nq, int D, int k);
 int dsp_knn_classify(const double *ref, const int32_t *ref_labels, int64_t Nr, const double *query,

@@ -65,7 +65,8 @@ def test_host_argument_checks(lib):
     assert f(*args(p2, 4)) == _hip.DSP_ERR_ARGS
     assert f(*args(p, 4, L=0)) == _hip.DSP_ERR_ARGS
     assert f(*args(p, 0)) == _hip.DSP_OK  # empty batch: nothing to launch
-    assert lib.dsp_knn_workspace_bytes(100, 100, 33, 5) == 0
+    assert lib.dsp_knn_workspace_bytes(100, 100, 4097, 5) == 0
+    assert lib.dsp_knn_workspace_bytes(100, 100, 33, 5) > 0  # high-dimensional screen
     assert lib.dsp_knn_workspace_bytes(100, 100, 15, 33) == 0
     assert lib.dsp_knn_workspace_bytes(100, 100, 15, 5) > 0
     k = lib.dsp_knn_classify

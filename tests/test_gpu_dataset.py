@@ -131,3 +131,26 @@ def test_extract_both_matches_oracle_padded(dataset_dir):
         assert not seq[i, n:].any()
     _, _, seq3, _ = d.extract_both(1102, 441, "hamming", use_only_energy_zcr=False)
     assert seq3.shape[2] == 3 and np.array_equal(seq3[:, :, [0, 2]], seq)
+
+
+def test_compare_feature_methods(dataset_dir):
+    """compare_feature_methods.compare: the reference's three classifiers on both feature sets,
+    KNN on the flattened sequences included (device KNN at D = 2 x max_frames), in the
+    reference's result shape; KNN's sequence accuracy equals the oracle KNN on the same split."""
+    import compare_feature_methods as cfm
+    from sklearn.model_selection import train_test_split
+    from src.feature_extraction import normalize_features
+    res = cfm.compare(dataset_dir)
+    assert set(res) == {"KNN", "SVM", "Decision Tree"}
+    for r in res.values():
+        assert 0.0 <= r["statistical"] <= 1.0 and 0.0 <= r["sequence"] <= 1.0
+        assert r["diff"] == r["sequence"] - r["statistical"]
+    _, X_seq, y, _ = cfm.load_both_methods(dataset_dir)
+    X = X_seq.reshape(len(X_seq), -1)
+    assert X.shape[1] > 32
+    tr, te, ytr, yte = train_test_split(X, y, test_size=0.2, random_state=42, stratify=y)
+    tr, m, sd = normalize_features(tr)
+    te, _, _ = normalize_features(te, m, sd)
+    classes, codes = np.unique(ytr, return_inverse=True)
+    _, _, pred = oracle.knn(tr, codes.astype(np.int32), te, 3, n_classes=len(classes))
+    assert res["KNN"]["sequence"] == float(np.mean(classes[pred] == yte))

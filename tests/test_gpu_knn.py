@@ -40,6 +40,28 @@ def test_knn_vs_oracle(Nr, Nq, D, k):
     assert np.array_equal(p1.cpu().numpy(), p0)
 
 
+@pytest.mark.parametrize("Nr,Nq,D,k", [(2000, 300, 198, 3), (1500, 500, 100, 5), (700, 200, 33, 1),
+                                      (500, 100, 1000, 12)])
+def test_knn_high_dim_vs_oracle(Nr, Nq, D, k):
+    """D > 32 (the sequence method's flattened features): chunked direct-form screen, fp64 re-rank;
+    indices, distances and votes bit-exact against the oracle (sklearn semantics)."""
+    from src.pipeline import knn_classify
+    rng = np.random.default_rng(Nr + D)
+    centres = rng.standard_normal((6, D))
+    y = rng.integers(0, 6, Nr).astype(np.int32)
+    X = centres[y] + 0.8 * rng.standard_normal((Nr, D))
+    Q = centres[rng.integers(0, 6, Nq)] + 0.8 * rng.standard_normal((Nq, D))
+    i0, d0, p0 = oracle.knn(X, y, Q, k, n_classes=6)
+    i1, d1, p1 = knn_classify(X, y, Q, k)
+    assert np.array_equal(i1.cpu().numpy(), i0)
+    assert np.array_equal(d1.cpu().numpy(), d0)
+    assert np.array_equal(p1.cpu().numpy(), p0)
+    # self-query exclusion on the high-dimensional path
+    i0, d0, _ = oracle.knn(X, y, X[:200], k, n_classes=6, self_offset=0)
+    i1, d1, _ = knn_classify(X, y, X[:200], k, self_offset=0)
+    assert np.array_equal(i1.cpu().numpy(), i0) and np.array_equal(d1.cpu().numpy(), d0)
+
+
 def test_knn_duplicates_force_fallback():
     """Exact duplicate rows make fp32 screening ties: the fp64 fallback must resolve them."""
     from src.pipeline import knn_classify
