@@ -32,6 +32,7 @@ static constexpr int KNN_RU = 4;     // rows x queries per unrolled step of the 
 #ifndef DSP_KNN_QP
 #define DSP_KNN_QP 2
 #endif
+
 static constexpr int KNN_QP = DSP_KNN_QP;  // queries per screening thread
 
 // mode 0: plain rows (v, 0 ...); mode 1 (reference, expanded form): (-2 v, 0 ..., |v|^2);
