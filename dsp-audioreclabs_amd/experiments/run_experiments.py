@@ -79,14 +79,20 @@ class SpeechRecognitionExperiment:
         return res
 
     def experiment_window_comparison(self):
-        res = {}
+        """:332-393 -> {window_type: {classifier: evaluate() results}} for KNN and SVM (the
+        reference's MLP entry is the out-of-scope torch MLP).  Every window re-runs load_dataset,
+        i.e. one fused launch over the HBM-resident PCM."""
+        window_results = {}
+        classifiers = {'KNN': ('knn', {'n_neighbors': config.KNN_N_NEIGHBORS}),
+                       'SVM': ('svm', {'C': config.SVM_C})}
         for w in config.WINDOW_TYPES:
             self.load_dataset(window_type=w)
             X_tr, X_te, y_tr, y_te = self.split_normalize()
-            r = self.train_and_evaluate_classifier('knn', X_tr, X_te, y_tr, y_te, n_neighbors=config.KNN_N_NEIGHBORS)
-            res[w] = float(r["accuracy"])
-        self._save("exp2_window_comparison", res)
-        return res
+            window_results[w] = {name: self.train_and_evaluate_classifier(kind, X_tr, X_te, y_tr, y_te, **params)
+                                 for name, (kind, params) in classifiers.items()}
+        self._save("exp2_window_comparison",
+                   {w: {c: float(r['accuracy']) for c, r in res.items()} for w, res in window_results.items()})
+        return window_results
 
     def _save(self, name, obj):
         d = os.path.join(self.results_dir, name)

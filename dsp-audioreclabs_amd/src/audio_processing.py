@@ -274,7 +274,7 @@ def endpoint_detection(audio_data, frame_length, frame_shift,
     x = _dev(audio_data)
     n = x.numel()
     if n < frame_length:
-        return 0, n, [], []
+        return 0, n, np.array([]), np.array([])
     nfr = (n - frame_length) // frame_shift + 1
     fr = x.unfold(0, frame_length, frame_shift)[:nfr]
     E = (fr * fr).sum(dim=1).cpu().numpy()
@@ -286,7 +286,7 @@ def endpoint_detection(audio_data, frame_length, frame_shift,
     t1 = speech_e * energy_high_ratio
     hi = np.nonzero(E > t1)[0]
     if hi.size == 0:
-        return 0, n, list(E), list(Z)
+        return 0, n, E, Z
     n3, n4 = int(hi[0]), int(hi[-1])
     t2 = noise_e + (speech_e - noise_e) * energy_low_ratio
     n2 = 0
@@ -311,4 +311,4 @@ def endpoint_detection(audio_data, frame_length, frame_shift,
         if Z[i] <= tz:
             n6 = i - 1
             break
-    return n1 * frame_shift, min(n6 * frame_shift + frame_length, n), list(E), list(Z)
+    return n1 * frame_shift, min(n6 * frame_shift + frame_length, n), E, Z

@@ -161,3 +161,12 @@ def test_load_dataset_batched(tmp_path):
     res = exp.experiment_classifier_comparison("hamming", classifiers={"KNN": ("knn", {"n_neighbors": 3})})
     assert 0.0 <= res["KNN"]["accuracy"] <= 1.0
     assert os.path.exists(tmp_path / "results" / "exp1_classifier_comparison" / "results.json")
+    # experiment_window_comparison: {window: {'KNN', 'SVM'}} (run_experiments.py:332-393)
+    wres = exp.experiment_window_comparison()
+    assert set(wres) == {"rectangular", "hamming", "hanning"}
+    for w, r in wres.items():
+        assert set(r) == {"KNN", "SVM"} and all(0.0 <= v["accuracy"] <= 1.0 for v in r.values())
+    # run.py with no --experiment runs 'all' (run.py:10-135 default)
+    import run
+    assert run.main(["--data-dir", str(tmp_path), "--results-dir", str(tmp_path / "r2")]) == 0
+    assert os.path.exists(tmp_path / "r2" / "exp2_window_comparison" / "results.json")
