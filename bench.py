@@ -263,7 +263,9 @@ def knn_leg(args, dev, world):
     """BASELINE configs[4] beside the headline metric: exact k-NN (KNeighborsClassifier
     semantics) of every one of --knn-ref synthetic z-scored 15-d vectors against all of them
     (self excluded), queries sharded over the ranks, results gathered (one RCCL all-gather).
-    Not part of ``value``; reported as its own object with its VALU roofline (45 flop per pair)."""
+    Not part of ``value``; reported as its own object with its fp32 roofline: 45 algorithmic flop per
+    pair (15 sub + 15 mul + 15 add) against 157.3 TF/s, the fp32 peak of both the matrix cores
+    (v_mfma_f32_16x16x4_f32, the screen's distances) and the VALU."""
     import torch
     import torch.distributed as dist
     from src.distributed import knn_sharded
@@ -298,7 +300,7 @@ def knn_leg(args, dev, world):
     return {"metric": "k-NN pairs/s (15-d, exact, k=%d, self-query, gathered)" % args.knn_k,
             "value": round(pairs / t, 1), "unit": "pairs/s", "ms": round(t * 1e3, 4),
             "ref": n, "queries": n, "queries_per_rank": -(-n // world),
-            "roofline": {"bound": "valu", "achieved": round(tf, 2), "peak": 157.3 * world, "unit": "TFLOP/s",
+            "roofline": {"bound": "mfma-f32", "achieved": round(tf, 2), "peak": 157.3 * world, "unit": "TFLOP/s",
                          "frac": round(tf / (157.3 * world), 4), "flop_per_pair": 45,
                          "note": "whole-job wall time incl. conversion, merge and the result all-gather"},
             "data": "synthetic z-scored 15-d vectors around 10 class centres"}
@@ -364,7 +366,8 @@ def cpu_baseline(fx, batch, L, S, window, vad, budget_s):
                       "cgroup quota %s); 1 thread: %.4g frames/s"
                       % (reps, C, total_t, threads, visible, quota, one),
             "parity_on_sample": {"clips": C, "start_end_exact": se_ok, "n_frames_exact": nf_ok,
-                                 "feat_max_rel_err": float(np.nanmax(rel))}}
+                                 "feat_max_rel_err": float(np.nanmax(rel)),
+                                 "feat_cells_over_1e-5_rel": int(np.nansum(rel > 1e-5))}}
 
 
 if __name__ == "__main__":

@@ -684,7 +684,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                 s2 = dpp_quad_sum64(s2);
                 zc = dpp_quad_reduce(zc, OpAdd());
                 if (act && lq == 0) {
-                    c.rank[f] = 0;
+                    if (!FAST) c.rank[f] = 0;
                     c.vE[f] = EXACT ? np_energy_exact(clip_g, f * S, L, mq, Mp)
                                     : energy_from_moments(s2, s1, L, t0, mq - (double)t0, invM2);
                     c.vZ[f] = zc;
@@ -709,6 +709,10 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                     // element is the one holding that high half, or, when several do, the one of the
                     // right rank among them by the full key
                     if (wid == 0) {
+                        // the workgroup's critical path (p90, then the scan) runs on this one wave:
+                        // it takes issue priority over the co-resident workgroup's waves until the
+                        // decisions are made (2% at 100k clips)
+                        __builtin_amdgcn_s_setprio(2);
                         const unsigned long long f0 = lane < nv ? dkey(c.vE[lane]) : ~0ull;
                         const unsigned long long f1 = lane + 64 < nv ? dkey(c.vE[lane + 64]) : ~0ull;
                         const unsigned h0 = (unsigned)(f0 >> 32), h1 = (unsigned)(f1 >> 32);
@@ -760,6 +764,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
         if (wid == 0) {
             const int flag = vad_scan<!EXACT, FAST>(p, c, nv, lane);
             if (lane == 0) sh->exact = (!EXACT && Mp > 0.0) ? flag : 0;
+            __builtin_amdgcn_s_setprio(0);
         }
         __syncthreads();
         if (!EXACT && sh->exact) {  // near tie: redo in numpy's exact order after the loop
@@ -887,12 +892,13 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
             // wave q alone handles sequence q (E, M, ZCR): lanes hold v[lane], v[lane + 64]; the
             // order statistics by ballot ranks over readlane'd candidates, then mean / std (fp64 sums)
             // and max / min -- no barrier
-            if (wid < 6) {
-                const int q = wid % 3;
+            // six jobs (median / moments of E, M, ZCR) over the waves
+            for (int job = wid; job < 6; job += NWAVE) {
+                const int q = job % 3;
                 auto get = [&](int j) -> float { return q == 0 ? c.fE[j] : q == 1 ? c.fM[j] : (float)c.fZ[j]; };
                 const bool in0 = lane < F, in1 = lane + 64 < F;
                 const float x0 = in0 ? get(lane) : 0.f, x1 = in1 ? get(lane + 64) : 0.f;
-                if (wid < 3) {  // median by an in-wave bitonic sort
+                if (job < 3) {  // median by an in-wave bitonic sort
                     unsigned a[2] = {in0 ? fkey(x0) : ~0u, in1 ? fkey(x1) : ~0u};
                     float v0, v1;
                     if (F <= 64) {
@@ -912,7 +918,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                     }
                     if (lane == 0) featb[5 * q + 4] = (float)med;
                 }
-                if (wid >= 3) {  // mean, population std (fp64 sums), max, min
+                if (job >= 3) {  // mean, population std (fp64 sums), max, min
                     const double s = wave_sum((in0 ? (double)x0 : 0.0) + (in1 ? (double)x1 : 0.0));
                     const float mx = wave_reduce(fmaxf(in0 ? x0 : -INFINITY, in1 ? x1 : -INFINITY), OpMax());
                     const float mn = wave_reduce(fminf(in0 ? x0 : INFINITY, in1 ? x1 : INFINITY), OpMin());
@@ -1214,7 +1220,7 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     // clips blockIdx, blockIdx + grid, ...; the compile-time layout whenever the launch fits it
     const bool fast = extract_fast_fits((int)max_len, frame_length, frame_shift);
     const size_t lds_launch = fast ? (size_t)extract_carve_fast().total : lds;
-    const int per_cu = lds_launch <= EXTRACT_LDS_SHARED ? 2 : 1;
+    const int per_cu = std::max(1, std::min<int>(EXTRACT_WG_PER_CU, (int)(EXTRACT_LDS_LIMIT / lds_launch)));
     const int slots = per_cu * num_cus;
     // at most EXTRACT_DEFER_CAP clips per workgroup and launch, so every near tie fits the
     // workgroup's redo list (larger batches: consecutive launches on the stream)

@@ -14,9 +14,13 @@
 #ifndef EXTRACT_RREG
 #define EXTRACT_RREG 3                   // 32-sample words per thread held in registers
 #endif
+#ifndef EXTRACT_WG_PER_CU
+#define EXTRACT_WG_PER_CU 2              // resident workgroups per CU the register budget allows
+#endif
 #define EXTRACT_LDS_LIMIT (160 * 1024)   // one CU
-#define EXTRACT_LDS_SHARED (80 * 1024)   // per workgroup when two share a CU
+#ifndef EXTRACT_DEFER_CAP
 #define EXTRACT_DEFER_CAP 256            // near-tie clips one workgroup can redo exactly
+#endif
 #define EXTRACT_SHARED_BYTES 512         // sizeof(dsp::Shared) rounded up (static_assert'ed)
 #define EXTRACT_WPAD 8                   // zero window entries on each side of the window table
 // floats per shifted window copy: copy r holds w[m - WPAD - r] at m (zero outside [0, L)), so
@@ -30,7 +34,8 @@ struct ExtractCarve {
 
 // Region offsets from the capacities: nwmax 32-sample words (incl. the alignment lead), nvcap VAD
 // frames, fcap feature frames, wrow floats per shifted window copy, per_wg deferred clips.
-__host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvcap, int fcap, int wrow, int per_wg)
+__host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvcap, int fcap, int wrow, int per_wg,
+                                                              bool rank = true)
 {
     ExtractCarve c{};
     int o = 0;
@@ -52,7 +57,7 @@ __host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvc
     DSP_TAKE(fE, 4 * c.fcap);
     DSP_TAKE(fM, 4 * c.fcap);
     DSP_TAKE(fZ, 4 * c.fcap);
-    DSP_TAKE(rank, 4 * (c.nvcap > 3 * c.fcap ? c.nvcap : 3 * c.fcap));
+    DSP_TAKE(rank, rank ? 4 * (c.nvcap > 3 * c.fcap ? c.nvcap : 3 * c.fcap) : 0);  // long clips only
     DSP_TAKE(pS2, 16 * c.nvcap);  // partial-word moments at the two ends of each VAD frame
     DSP_TAKE(pS1, 8 * c.nvcap);
     DSP_TAKE(defer, 4 * per_wg);
@@ -75,12 +80,14 @@ __host__ __device__ inline ExtractCarve extract_carve(int ncap, int L, int S, in
 // window rows of <= EXTRACT_FAST_WROW floats (frame_length <= 1256).
 #define EXTRACT_FAST_NV 128
 #define EXTRACT_FAST_NF 128
+#ifndef EXTRACT_FAST_WROW
 #define EXTRACT_FAST_WROW 1280
+#endif
 #define EXTRACT_FAST_NWORD (EXTRACT_THREADS * EXTRACT_RREG)
 __host__ __device__ constexpr ExtractCarve extract_carve_fast()
 {
     return extract_carve_caps(EXTRACT_FAST_NWORD + 1, EXTRACT_FAST_NV, EXTRACT_FAST_NF, EXTRACT_FAST_WROW,
-                              EXTRACT_DEFER_CAP);
+                              EXTRACT_DEFER_CAP, false);
 }
 __host__ __device__ inline bool extract_fast_fits(int ncap, int L, int S)
 {

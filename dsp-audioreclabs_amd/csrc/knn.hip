@@ -1,25 +1,30 @@
-// knn.hip -- exact k-nearest-neighbour classification for gfx950 (CDNA4), VALU only.
+// knn.hip -- exact k-nearest-neighbour classification for gfx950 (CDNA4).
 //
 // Replaces KNeighborsClassifier(n_neighbors=k).fit/predict/kneighbors as used by
 // src/models.py:33-35,52-58 (sklearn 1.7.2: algorithm='auto' -> kd_tree, minkowski p=2,
 // uniform weights, scipy.stats.mode vote).
 //
 // Pipeline (all stream-ordered, no host sync):
-//   1. knn_convert    fp64 [N,D] -> fp32 [N,DP] zero-padded rows (+ max row norm^2, for the bound)
-//   2. knn_screen     grid (query block of 256, reference split): each thread owns one query,
-//                     streams its split's reference rows through LDS tiles and keeps the KC
-//                     smallest fp32 squared distances (KC = k + 4 slack) in registers.  The
-//                     [Nq x Nr] distance matrix is never materialised.
-//   3. knn_merge      one thread per query: re-ranks every surviving candidate with the
-//                     reference's own fp64 distance (sequential sum of squared differences, no
-//                     FMA -- sklearn euclidean_rdist), keeps the k best by (distance, index), and
-//                     certifies that no screened-out row can beat the k-th; otherwise the query
-//                     goes on a fallback list.
-//   4. knn_fallback   one workgroup per listed query: exhaustive fp64 scan.
-//   5. vote           majority label, smallest label on ties (scipy.stats.mode).
+//   1. knn_convert      fp64 [N,D] -> fp32 [N,DP] zero-padded rows (+ max row norm^2, for the
+//                       bound); D < DP: expanded form, references (-2 r, |r|^2), queries (q, 1)
+//   2. screen           grid (query block, reference split); each query keeps the KC smallest
+//                       fp32 squared distances (KC = k + 3 slack, rounded up) of its split; the
+//                       [Nq x Nr] distance matrix is never materialised:
+//        knn_screen_mfma  D < DP (the 15-d features): |q|^2 + q'.r' on v_mfma_f32_16x16x4_f32
+//        knn_screen       D = 16 or 32: direct form (q - r)^2 on the VALU
+//        knn_screen_hd    D > 32 (flattened sequences): direct form in chunks of 16 dimensions
+//   3. knn_merge        one thread per query: re-ranks every surviving candidate with the
+//                       reference's own fp64 distance (sequential sum of squared differences, no
+//                       FMA -- sklearn euclidean_rdist), keeps the k best by (distance, index), and
+//                       certifies that no screened-out row can beat the k-th; otherwise the query
+//                       goes on a fallback list.
+//   4. knn_fallback     one workgroup per listed query: exhaustive fp64 scan.
+//   5. vote             majority label, smallest label on ties (scipy.stats.mode).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+
+#include <algorithm>
 
 #include "dsp_audiorec.h"
 
@@ -79,10 +84,11 @@ __device__ __forceinline__ void topk_insert(float (&dl)[KC], int (&il)[KC], floa
     dl[0] = fminf(d, dl[0]);
 }
 
-// QP queries per thread (queries q0 + tid + KNN_TQ * p): every 16-B LDS read of a reference row
-// feeds QP FMAs -- a broadcast ds_read_b128 costs the CU's LDS pipe 4 cycles, shared by 4 SIMDs,
-// so at one query per thread the screen is LDS-bound
-template <int DP, int KC, bool EXP, int QP>
+// Direct form sum (q - r)^2 on the VALU, for D = 16 and D = 32 (no spare column for the expanded
+// form of knn_screen_mfma).  QP queries per thread (queries q0 + tid + KNN_TQ * p): every 16-B LDS
+// read of a reference row feeds QP FMA chains -- a broadcast ds_read_b128 costs the CU's LDS pipe
+// 4 cycles, shared by 4 SIMDs, so at one query per thread the screen is LDS-bound
+template <int DP, int KC, int QP>
 __global__ __launch_bounds__(KNN_TQ) void knn_screen(const float *__restrict__ ref32, int64_t Nr,
                                                       const float *__restrict__ q32, int64_t Nq,
                                                       int64_t self_offset, int nsplit,
@@ -95,7 +101,7 @@ __global__ __launch_bounds__(KNN_TQ) void knn_screen(const float *__restrict__ r
     const int64_t per = (Nr + nsplit - 1) / nsplit;
     const int64_t r0 = (int64_t)sp * per, r1 = min(Nr, r0 + per);
     int64_t q[QP], self[QP];
-    float qv[QP][DP], qn[QP];
+    float qv[QP][DP];
     float dl[QP][KC];
     int il[QP][KC];
 #pragma unroll
@@ -103,9 +109,6 @@ __global__ __launch_bounds__(KNN_TQ) void knn_screen(const float *__restrict__ r
         q[p] = (int64_t)qb * KNN_TQ * QP + tid + KNN_TQ * p;
 #pragma unroll
         for (int c = 0; c < DP; c++) qv[p][c] = q[p] < Nq ? q32[q[p] * DP + c] : 0.f;
-        qn[p] = 0.f;  // expanded form: |q|^2 + sum q'_c r'_c, one FMA per dimension
-#pragma unroll
-        for (int c = 0; c < DP - 1; c++) qn[p] = fmaf(qv[p][c], qv[p][c], qn[p]);
         self[p] = (self_offset >= 0 && q[p] < Nq) ? self_offset + q[p] : -1;
 #pragma unroll
         for (int i = 0; i < KC; i++) {
@@ -132,24 +135,17 @@ __global__ __launch_bounds__(KNN_TQ) void knn_screen(const float *__restrict__ r
             for (int u = 0; u < RU; u++) {
                 const float4 *rv = reinterpret_cast<const float4 *>(tile + (j0 + u) * DP);  // rows >= nt are zero
 #pragma unroll
-                for (int p = 0; p < QP; p++) d[u][p] = EXP ? qn[p] : 0.f;
+                for (int p = 0; p < QP; p++) d[u][p] = 0.f;
 #pragma unroll
                 for (int c4 = 0; c4 < DP / 4; c4++) {
                     const float4 r = rv[c4];
 #pragma unroll
                     for (int p = 0; p < QP; p++) {
-                        if (EXP) {
-                            d[u][p] = fmaf(qv[p][4 * c4 + 0], r.x, d[u][p]);
-                            d[u][p] = fmaf(qv[p][4 * c4 + 1], r.y, d[u][p]);
-                            d[u][p] = fmaf(qv[p][4 * c4 + 2], r.z, d[u][p]);
-                            d[u][p] = fmaf(qv[p][4 * c4 + 3], r.w, d[u][p]);
-                        } else {
-                            float t;
-                            t = qv[p][4 * c4 + 0] - r.x; d[u][p] = fmaf(t, t, d[u][p]);
-                            t = qv[p][4 * c4 + 1] - r.y; d[u][p] = fmaf(t, t, d[u][p]);
-                            t = qv[p][4 * c4 + 2] - r.z; d[u][p] = fmaf(t, t, d[u][p]);
-                            t = qv[p][4 * c4 + 3] - r.w; d[u][p] = fmaf(t, t, d[u][p]);
-                        }
+                        float t;
+                        t = qv[p][4 * c4 + 0] - r.x; d[u][p] = fmaf(t, t, d[u][p]);
+                        t = qv[p][4 * c4 + 1] - r.y; d[u][p] = fmaf(t, t, d[u][p]);
+                        t = qv[p][4 * c4 + 2] - r.z; d[u][p] = fmaf(t, t, d[u][p]);
+                        t = qv[p][4 * c4 + 3] - r.w; d[u][p] = fmaf(t, t, d[u][p]);
                     }
                 }
             }
@@ -172,6 +168,151 @@ __global__ __launch_bounds__(KNN_TQ) void knn_screen(const float *__restrict__ r
                 cand_i[o + i] = il[p][i];
             }
         }
+}
+
+// Expanded-form screen on the matrix cores (D < DP, DP = 16 or 32): per 16 reference rows x 16
+// queries, DP / 4 v_mfma_f32_16x16x4_f32 accumulate |q|^2 + q'.r' -- bit for bit a k-ordered fp32
+// fmaf chain, so the error bound of the VALU screen holds unchanged.  A operand = reference rows
+// (lane l: row l & 15), B = queries (lane l: query l & 15), lane l's dimensions in MFMA j are
+// 16 (j / 4) + 4 (l >> 4) + (j & 3): one 16-B read per 4 MFMAs.  Result lane l: query l & 15,
+// rows 4 (l >> 4) + v, v = 0..3, so four lanes keep partial top-KC lists of each query.
+// Keeping the lists is the expensive part (an insertion costs the whole wave whenever one lane
+// makes one), so each 16-row step first compares its distances with the query's threshold -- the
+// smallest of the four lists' last entries: a row at or above it cannot be among the KC nearest
+// of the union -- and inserts only when some lane has a distance below it.  Padding rows carry an
+// infinite |r|^2 (distance +inf); the query's own row (self_offset) is masked only in the steps
+// that can hold one of the wave's 32 own rows.
+static constexpr int MQ_W = 2;                         // waves per workgroup
+// query tiles (16 queries) per wave: two while the lists are short, one for long lists (k > 13)
+__host__ __device__ constexpr int mq_tiles(int KC) { return KC <= 16 ? 2 : 1; }
+__host__ __device__ constexpr int mq_qpb(int KC) { return 16 * mq_tiles(KC) * MQ_W; }  // queries per workgroup
+static constexpr int MQ_TR = 256;                      // reference rows per LDS tile
+__host__ __device__ constexpr int mq_stride(int DP) { return DP + 4; }  // conflict-free 16-B reads
+typedef float mq_f4 __attribute__((ext_vector_type(4)));
+template <int DP, int KC>
+__global__ __launch_bounds__(64 * MQ_W) void knn_screen_mfma(const float *__restrict__ ref32, int64_t Nr,
+                                                           const float *__restrict__ q32, int64_t Nq,
+                                                           int64_t self_offset, int nsplit,
+                                                           float *__restrict__ cand_d, int *__restrict__ cand_i)
+{
+    constexpr int RS = mq_stride(DP), NJ = DP / 4, NV = DP / 16;
+    constexpr int MQ_T = mq_tiles(KC), MQ_QPB = mq_qpb(KC);
+    __shared__ __attribute__((aligned(16))) float tile[MQ_TR * RS];
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int col = lane & 15, rg = lane >> 4;
+    const int sp = blockIdx.y;
+    const int64_t per = (Nr + nsplit - 1) / nsplit;
+    const int64_t r0 = (int64_t)sp * per, r1 = min(Nr, r0 + per);
+    const int64_t wq0 = (int64_t)blockIdx.x * MQ_QPB + wid * MQ_T * 16;  // the wave's first query
+    // rows that can be one of the wave's own queries (self_offset >= 0): [slo, slo + 16 MQ_T)
+    const int64_t slo = self_offset >= 0 ? self_offset + wq0 : INT64_MIN / 2;
+    int64_t q[MQ_T], self[MQ_T];
+    float qb[MQ_T][NJ], qn[MQ_T], tau[MQ_T];
+    float dl[MQ_T][KC];
+    int il[MQ_T][KC];
+#pragma unroll
+    for (int t = 0; t < MQ_T; t++) {
+        q[t] = wq0 + t * 16 + col;
+        const float *qr = q32 + (q[t] < Nq ? q[t] : 0) * DP;
+        float n = 0.f;  // |q|^2 as the VALU screen computes it (fmaf chain over the real columns)
+#pragma unroll
+        for (int c = 0; c < DP - 1; c++) n = fmaf(qr[c], qr[c], n);
+        qn[t] = n;
+#pragma unroll
+        for (int h = 0; h < NV; h++) {
+            const float4 v = *reinterpret_cast<const float4 *>(qr + 16 * h + 4 * rg);
+            qb[t][4 * h] = v.x;
+            qb[t][4 * h + 1] = v.y;
+            qb[t][4 * h + 2] = v.z;
+            qb[t][4 * h + 3] = v.w;
+        }
+        self[t] = (self_offset >= 0 && q[t] < Nq) ? self_offset + q[t] : -1;
+        tau[t] = INFINITY;
+#pragma unroll
+        for (int i = 0; i < KC; i++) {
+            dl[t][i] = INFINITY;
+            il[t][i] = -1;
+        }
+    }
+    for (int64_t t0 = r0; t0 < r1; t0 += MQ_TR) {
+        const int nt = (int)min((int64_t)MQ_TR, r1 - t0);
+        __syncthreads();
+        for (int e = tid; e < MQ_TR * DP / 4; e += 64 * MQ_W) {
+            const int row = e / (DP / 4), c4 = e % (DP / 4);
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (row < nt)
+                v = reinterpret_cast<const float4 *>(ref32 + (t0 + row) * DP)[c4];
+            else if (c4 == DP / 4 - 1)
+                v.w = INFINITY;  // |r|^2 of a padding row: distance +inf
+            *reinterpret_cast<float4 *>(tile + row * RS + 4 * c4) = v;
+        }
+        __syncthreads();
+        const int nt16 = (nt + 15) & ~15;
+        for (int s0 = 0; s0 < nt16; s0 += 16) {
+            float a[NJ];
+#pragma unroll
+            for (int h = 0; h < NV; h++) {
+                const float4 v = *reinterpret_cast<const float4 *>(tile + (s0 + col) * RS + 16 * h + 4 * rg);
+                a[4 * h] = v.x;
+                a[4 * h + 1] = v.y;
+                a[4 * h + 2] = v.z;
+                a[4 * h + 3] = v.w;
+            }
+            mq_f4 acc[MQ_T];
+#pragma unroll
+            for (int t = 0; t < MQ_T; t++) acc[t] = mq_f4{qn[t], qn[t], qn[t], qn[t]};
+#pragma unroll
+            for (int j = 0; j < NJ; j++)
+#pragma unroll
+                for (int t = 0; t < MQ_T; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], qb[t][j], acc[t], 0, 0, 0);
+            const int64_t rb = t0 + s0;  // the step's first row
+            if (rb < slo + 16 * MQ_T && rb + 16 > slo)  // wave-uniform: a query's own row may be here
+                for (int t = 0; t < MQ_T; t++)
+                    for (int v = 0; v < 4; v++)
+                        if (rb + 4 * rg + v == self[t]) acc[t][v] = INFINITY;
+            for (int t = 0; t < MQ_T; t++) {
+                bool c[4];
+#pragma unroll
+                for (int v = 0; v < 4; v++) c[v] = acc[t][v] < tau[t];
+                if (__builtin_amdgcn_ballot_w64(c[0] | c[1] | c[2] | c[3])) {
+#pragma unroll
+                    for (int v = 0; v < 4; v++)
+                        if (c[v]) topk_insert<KC>(dl[t], il[t], acc[t][v], (int)(rb + 4 * rg + v));
+                    float th = dl[t][KC - 1];
+                    th = fminf(th, __shfl_xor(th, 16, 64));
+                    th = fminf(th, __shfl_xor(th, 32, 64));
+                    tau[t] = th;
+                }
+            }
+        }
+    }
+    // the four partial lists of each query (lanes col, col + 16, col + 32, col + 48; disjoint
+    // rows) -> one, by a butterfly over lane ^ 16 and lane ^ 32
+#pragma unroll
+    for (int t = 0; t < MQ_T; t++) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int m = 16 << h;
+            float pd[KC];
+            int pi[KC];
+#pragma unroll
+            for (int i = 0; i < KC; i++) {
+                pd[i] = __shfl_xor(dl[t][i], m, 64);
+                pi[i] = __shfl_xor(il[t][i], m, 64);
+            }
+#pragma unroll
+            for (int i = 0; i < KC; i++)
+                if (pi[i] >= 0) topk_insert<KC>(dl[t], il[t], pd[i], pi[i]);
+        }
+        if (rg == 0 && q[t] < Nq) {
+            const size_t o = ((size_t)sp * Nq + q[t]) * KC;
+#pragma unroll
+            for (int i = 0; i < KC; i++) {
+                cand_d[o + i] = dl[t][i];
+                cand_i[o + i] = il[t][i];
+            }
+        }
+    }
 }
 
 // High-dimensional rows (D > 32: the sequence method's flattened (E, ZCR) sequences,
@@ -490,6 +631,7 @@ struct KnnLayout {
     int DP, KC, nsplit;
     bool exp;  // expanded-form screening (a spare padded column holds |r|^2)
     bool hd;   // D > 32: chunked direct-form screen (knn_screen_hd)
+    bool mfma; // expanded form on the matrix cores (knn_screen_mfma)
 };
 
 static constexpr int KNN_DMAX = 4096;
@@ -501,6 +643,26 @@ int pick_kc(int k)
     if (need <= 16) return 16;
     if (need <= 24) return 24;
     return 36;
+}
+
+// MFMA screen: reference splits.  Every workgroup of the grid is resident at once, so a CU's time
+// is (rows per split + a split's list warm-up, ~16k rows) x its waves, and a CU saturates at
+// about two waves per SIMD:  T(s) = (Nr / s + 16k) * max(waves on the busiest CU, 8).
+int pick_nsplit_mfma(int64_t Nr, int64_t Nq, int qpb, int cus)
+{
+    const int64_t qblocks = (Nq + qpb - 1) / qpb;
+    const int64_t maxs = std::max<int64_t>(1, std::min<int64_t>(64, (Nr + dsp::MQ_TR - 1) / dsp::MQ_TR));
+    int best = 1;
+    double best_t = 1e300;
+    for (int64_t s = 1; s <= maxs; s++) {
+        const int64_t waves = (qblocks * s + cus - 1) / cus * dsp::MQ_W;
+        const double t = ((double)Nr / (double)s + 16384.0) * (double)std::max<int64_t>(waves, 8);
+        if (t < best_t * (1.0 - 1e-9)) {
+            best_t = t;
+            best = (int)s;
+        }
+    }
+    return best;
 }
 
 int pick_nsplit(int64_t Nr, int64_t Nq, int qpb)
@@ -523,6 +685,20 @@ int pick_nsplit(int64_t Nr, int64_t Nq, int qpb)
 
 size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// CUs of the current device, cached
+int device_cus()
+{
+    static int cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cache[dev] == 0) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+        cache[dev] = cus;
+    }
+    return cache[dev];
+}
+
 KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
 {
     KnnLayout l;
@@ -530,7 +706,9 @@ KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
     l.DP = D <= 16 ? 16 : D <= 32 ? 32 : (D + 15) & ~15;
     l.exp = !l.hd && D < l.DP;
     l.KC = pick_kc(k);
-    l.nsplit = pick_nsplit(Nr, Nq, l.hd ? dsp::KNN_TQ : dsp::KNN_TQ * dsp::KNN_QP);
+    l.mfma = l.exp;  // every expanded-form screen runs on the matrix cores
+    l.nsplit = l.mfma ? pick_nsplit_mfma(Nr, Nq, dsp::mq_qpb(l.KC), device_cus())
+                      : pick_nsplit(Nr, Nq, l.hd ? dsp::KNN_TQ : dsp::KNN_TQ * dsp::KNN_QP);
     size_t o = 0;
     l.ref32 = o; o += al((size_t)Nr * l.DP * 4);
     l.q32 = o;   o += al((size_t)Nq * l.DP * 4);
@@ -542,15 +720,11 @@ KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
 }
 
 template <int DP, int KC>
-void launch_screen(dim3 g, hipStream_t s, bool exp, const float *r, int64_t Nr, const float *q, int64_t Nq,
-                   int64_t self, int nsplit, float *cd, int *ci)
+void launch_screen(dim3 g, hipStream_t s, const float *r, int64_t Nr, const float *q, int64_t Nq, int64_t self,
+                   int nsplit, float *cd, int *ci)
 {
-    if (exp)
-        hipLaunchKernelGGL((dsp::knn_screen<DP, KC, true, dsp::KNN_QP>), g, dim3(dsp::KNN_TQ), 0, s, r, Nr, q,
-                           Nq, self, nsplit, cd, ci);
-    else
-        hipLaunchKernelGGL((dsp::knn_screen<DP, KC, false, dsp::KNN_QP>), g, dim3(dsp::KNN_TQ), 0, s, r, Nr, q,
-                           Nq, self, nsplit, cd, ci);
+    hipLaunchKernelGGL((dsp::knn_screen<DP, KC, dsp::KNN_QP>), g, dim3(dsp::KNN_TQ), 0, s, r, Nr, q, Nq,
+                       self, nsplit, cd, ci);
 }
 
 template <int KC>
@@ -626,10 +800,20 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
             DSP_SCREEN_HD(8); DSP_SCREEN_HD(16); DSP_SCREEN_HD(24); DSP_SCREEN_HD(36);
 #undef DSP_SCREEN_HD
         }
+    } else if (l.mfma) {
+        const int qpb = dsp::mq_qpb(l.KC);
+        const dim3 g((unsigned)((Nq + qpb - 1) / qpb), (unsigned)l.nsplit), b(64 * dsp::MQ_W);
+#define DSP_SCREEN_MQ(DPV, KCV)                                                                   \
+    if (l.DP == DPV && l.KC == KCV)                                                               \
+    hipLaunchKernelGGL((dsp::knn_screen_mfma<DPV, KCV>), g, b, 0, s, ref32, Nr, q32, Nq, self_offset, \
+                       l.nsplit, cd, ci)
+        DSP_SCREEN_MQ(16, 8); DSP_SCREEN_MQ(16, 16); DSP_SCREEN_MQ(16, 24); DSP_SCREEN_MQ(16, 36);
+        DSP_SCREEN_MQ(32, 8); DSP_SCREEN_MQ(32, 16); DSP_SCREEN_MQ(32, 24); DSP_SCREEN_MQ(32, 36);
+#undef DSP_SCREEN_MQ
     } else {
         const dim3 g((unsigned)((Nq + dsp::KNN_TQ * dsp::KNN_QP - 1) / (dsp::KNN_TQ * dsp::KNN_QP)), (unsigned)l.nsplit);
 #define DSP_SCREEN(DPV, KCV)                                                                  \
-    if (l.DP == DPV && l.KC == KCV) launch_screen<DPV, KCV>(g, s, l.exp, ref32, Nr, q32, Nq, self_offset, \
+    if (l.DP == DPV && l.KC == KCV) launch_screen<DPV, KCV>(g, s, ref32, Nr, q32, Nq, self_offset, \
                                                             l.nsplit, cd, ci)
         DSP_SCREEN(16, 8); DSP_SCREEN(16, 16); DSP_SCREEN(16, 24); DSP_SCREEN(16, 36);
         DSP_SCREEN(32, 8); DSP_SCREEN(32, 16); DSP_SCREEN(32, 24); DSP_SCREEN(32, 36);

@@ -4,4 +4,4 @@
 set -e
 cd "$(dirname "$0")/../dsp-audioreclabs_amd/csrc"
 n=$1; shift
-/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -I../../include -Wall -Wno-unused-function "$@" extract.hip general.hip knn.hip -o ../lib/libdsp_audiorec_$n.so
+/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -I../../include -Wall -Wno-unused-function -mllvm -amdgpu-mfma-vgpr-form "$@" extract.hip general.hip knn.hip -o ../lib/libdsp_audiorec_$n.so
