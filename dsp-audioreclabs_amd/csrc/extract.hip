@@ -31,6 +31,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "dsp_audiorec.h"
 #include "extract_layout.h"
@@ -97,6 +98,8 @@ struct ExtractParams {
     float *seq;
     int ld_seq;
     unsigned long long *stamps;  // diagnostic build only (else null)
+    unsigned *queue;             // [0] clips claimed past the first G, [1] workgroups done; both
+                                 // zero at launch, the last workgroup out zeroes them again
     ExtractCarve cv;             // LDS layout, computed on the host (kernel arguments can be
                                  // re-read instead of being held in registers)
 };
@@ -112,7 +115,7 @@ struct Shared {
     double pa, pb;            // the two order statistics of the VAD energies around p90
     double noise_e, noise_z;  // VAD noise estimates (:189-195, :239-245)
     double oslo[3], oshi[3];  // order statistics (F-1)/2 and F/2 of E, M, ZCR (medians)
-    int n3, n1, n6, exact, j0, j1, ndefer;
+    int n3, n1, n6, exact, j0, j1, ndefer, next;
 };
 static_assert(sizeof(Shared) <= EXTRACT_SHARED_BYTES, "grow EXTRACT_SHARED_BYTES");
 
@@ -1116,20 +1119,32 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     __syncthreads();
     WG_CK(20);
 
-    // clips blockIdx.x, blockIdx.x + G, ...  The host splits launches so that no workgroup walks
-    // more than EXTRACT_DEFER_CAP clips: the near-tie list below can never overflow.
+    // Clip blockIdx.x first, then clips claimed from a launch-wide counter, so that workgroups
+    // whose clips run short take more of them (a static i, i + G, ... split ends on the slowest
+    // workgroup: 3.19-3.98 ms spread at 100 000 clips).  Thread 0 claims the next clip right after
+    // issuing the current clip's loads; the claim's latency hides behind the clip.  A workgroup
+    // claims only while its near-tie list has room for the current and the claimed clip, and the
+    // host keeps a launch at <= G * EXTRACT_DEFER_CAP / 2 clips, so the list never overflows and
+    // some workgroup can always claim what is left.
     short8 regs[NRV];
-    for (int i = blockIdx.x; i < p.B; i += G) {
+    for (int i = blockIdx.x; i < p.B;) {
         const ClipRef cur = clip_ref(p, i);
+        unsigned claim = 0x7fffffffu;
         if (!cur.ok) {
+            __syncthreads();  // everyone has read sh->next (the ok path has barriers in clip_body)
+            if (tid == 0) claim = (unsigned)G + __hip_atomic_fetch_add(p.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             write_bad_clip(p, i, tid);
-            continue;
+        } else {
+            issue_clip(regs, p, cur);
+            if (tid == 0 && sh->ndefer < EXTRACT_DEFER_CAP - 1)
+                claim = (unsigned)G + __hip_atomic_fetch_add(p.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            c.stamp_clip = i;
+            const bool done = clip_body<false, FAST>(p, c, i, cur, regs);
+            if (!done && tid == 0) c.defer[sh->ndefer++] = i;
         }
-        issue_clip(regs, p, cur);
-        c.stamp_clip = i;
-        const bool done = clip_body<false, FAST>(p, c, i, cur, regs);
-        if (!done && tid == 0) c.defer[sh->ndefer++] = i;
-        __syncthreads();  // LDS summaries are rewritten by the next clip
+        if (tid == 0) sh->next = (int)min(claim, 0x7fffffffu);
+        __syncthreads();  // LDS summaries are rewritten by the next clip; sh->next published
+        i = sh->next;
     }
     // near ties (rare): endpoint energies in numpy's exact float64 order
     __syncthreads();
@@ -1138,6 +1153,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
         const int j = c.defer[d];
         clip_exact<FAST>((const ExtractParams *)__builtin_amdgcn_kernarg_segment_ptr(), j);
         __syncthreads();
+    }
+    // the last workgroup out resets the queue for the next launch on the stream: every claim of
+    // every workgroup precedes its increment of the done count
+    if (tid == 0) {
+        const unsigned d = __hip_atomic_fetch_add(p.queue + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == (unsigned)G - 1) {
+            __hip_atomic_store(p.queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(p.queue + 1, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     WG_STAMP(22);
 }
@@ -1161,8 +1185,14 @@ extern "C" size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int f
     return c.total <= EXTRACT_LDS_LIMIT ? (size_t)c.total : 0;
 }
 
-// CU count per device (the persistent grid), cached on first use of each device
+// CU count per device (the persistent grid), cached on first use of each device, and per device
+// a pool of clip-queue counter pairs (ExtractParams::queue): launches take slots round robin, so
+// launches in flight on different streams use different counters
 static int g_num_cus[64];
+static constexpr int QUEUE_SLOTS = 1024;
+static_assert(EXTRACT_DEFER_CAP >= 2, "the claim rule keeps room for two clips");
+static unsigned *g_queue[64];
+static std::atomic<unsigned> g_queue_next{0};
 
 extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, int B,
                                     int64_t max_len, int frame_length, int frame_shift,
@@ -1186,6 +1216,11 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     if (g_num_cus[dev] == 0) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return DSP_ERR_HIP;
+        unsigned *q = nullptr;
+        if (hipMalloc((void **)&q, sizeof(unsigned) * 2 * QUEUE_SLOTS) != hipSuccess) return DSP_ERR_HIP;
+        if (hipMemset(q, 0, sizeof(unsigned) * 2 * QUEUE_SLOTS) != hipSuccess) return DSP_ERR_HIP;
+        if (hipDeviceSynchronize() != hipSuccess) return DSP_ERR_HIP;
+        g_queue[dev] = q;
         g_num_cus[dev] = prop.multiProcessorCount;
         (void)hipFuncSetAttribute((const void *)dsp::extract_kernel<true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
@@ -1222,9 +1257,10 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     const size_t lds_launch = fast ? (size_t)extract_carve_fast().total : lds;
     const int per_cu = std::max(1, std::min<int>(EXTRACT_WG_PER_CU, (int)(EXTRACT_LDS_LIMIT / lds_launch)));
     const int slots = per_cu * num_cus;
-    // at most EXTRACT_DEFER_CAP clips per workgroup and launch, so every near tie fits the
-    // workgroup's redo list (larger batches: consecutive launches on the stream)
-    const int64_t chunk = (int64_t)slots * EXTRACT_DEFER_CAP;
+    // at most EXTRACT_DEFER_CAP / 2 clips per workgroup and launch on average (see the claim rule
+    // in extract_kernel), so every near tie fits its workgroup's redo list (larger batches:
+    // consecutive launches on the stream)
+    const int64_t chunk = (int64_t)slots * (EXTRACT_DEFER_CAP / 2);
     for (int64_t b0 = 0; b0 < B; b0 += chunk) {
         dsp::ExtractParams q = p;
         const int nb = (int)std::min<int64_t>(chunk, B - b0);
@@ -1241,6 +1277,7 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
         if (seq) q.seq = seq + b0 * ld_seq * 3;
         if (q.stamps) q.stamps = p.stamps + 32 * b0;
         const int grid = nb < slots ? nb : slots;
+        q.queue = g_queue[dev] + 2 * (g_queue_next.fetch_add(1, std::memory_order_relaxed) % QUEUE_SLOTS);
         if (fast)
             hipLaunchKernelGGL(dsp::extract_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch, (hipStream_t)stream, q);
         else
