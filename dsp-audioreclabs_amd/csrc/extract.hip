@@ -37,6 +37,10 @@
 #include "extract_layout.h"
 #include "dsp_device.h"
 
+// issue the next clip's loads after R4 (the last phase reading global memory), overlapping R5
+#ifndef EXTRACT_PF_R5
+#define EXTRACT_PF_R5 1
+#endif
 #ifndef EXTRACT_R4_KV
 #define EXTRACT_R4_KV 9
 #endif
@@ -462,7 +466,7 @@ __device__ __forceinline__ void partial_moments(const short8 (&q)[4], int e0, in
 // at most 128 VAD and feature frames, so the long-clip paths drop out
 template <bool EXACT, bool FAST>
 __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, int i, const ClipRef &cur,
-                                          short8 (&regs)[NRV])
+                                          short8 (&regs)[NRV], unsigned claim = 0x7fffffffu)
 {
     Shared *sh = c.sh;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -884,7 +888,15 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     }
     if (!FAST && F > 128)
         for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
+    if constexpr (!EXACT && EXTRACT_PF_R5)
+        if (tid == 0) sh->next = (int)min(claim, 0x7fffffffu);  // claimed at the clip's start
     __syncthreads();
+    if constexpr (!EXACT && EXTRACT_PF_R5) {
+        // regs are dead since R2: the next clip's words load while R5 runs (unconditional, a
+        // clip_none() reads zeros, so the compiler's vmcnt bookkeeping stays exact)
+        const int nx = sh->next;
+        issue_clip(regs, p, nx < p.B ? clip_ref(p, nx) : clip_none());
+    }
     STAMP(i, 5);
 
     // ---- R5: 15-d statistics (compute_statistics x 3, fe.py:46-62) ------------------------
@@ -1127,6 +1139,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     // host keeps a launch at <= G * EXTRACT_DEFER_CAP / 2 clips, so the list never overflows and
     // some workgroup can always claim what is left.
     short8 regs[NRV];
+    bool inflight = false;  // regs already hold clip i's loads (EXTRACT_PF_R5)
     for (int i = blockIdx.x; i < p.B;) {
         const ClipRef cur = clip_ref(p, i);
         unsigned claim = 0x7fffffffu;
@@ -1134,13 +1147,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
             __syncthreads();  // everyone has read sh->next (the ok path has barriers in clip_body)
             if (tid == 0) claim = (unsigned)G + __hip_atomic_fetch_add(p.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             write_bad_clip(p, i, tid);
+            inflight = false;
         } else {
-            issue_clip(regs, p, cur);
+            if (!inflight) issue_clip(regs, p, cur);
             if (tid == 0 && sh->ndefer < EXTRACT_DEFER_CAP - 1)
                 claim = (unsigned)G + __hip_atomic_fetch_add(p.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             c.stamp_clip = i;
-            const bool done = clip_body<false, FAST>(p, c, i, cur, regs);
+            const bool done = clip_body<false, FAST>(p, c, i, cur, regs, claim);
             if (!done && tid == 0) c.defer[sh->ndefer++] = i;
+            inflight = EXTRACT_PF_R5 && done;  // a deferred clip returns before R4
         }
         if (tid == 0) sh->next = (int)min(claim, 0x7fffffffu);
         __syncthreads();  // LDS summaries are rewritten by the next clip; sh->next published
