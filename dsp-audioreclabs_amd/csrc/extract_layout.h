@@ -19,7 +19,7 @@
 #endif
 #define EXTRACT_LDS_LIMIT (160 * 1024)   // one CU
 #ifndef EXTRACT_DEFER_CAP
-#define EXTRACT_DEFER_CAP 256            // near-tie clips one workgroup can redo exactly
+#define EXTRACT_DEFER_CAP 512            // near-tie clips one workgroup can redo exactly
 #endif
 #define EXTRACT_SHARED_BYTES 512         // sizeof(dsp::Shared) rounded up (static_assert'ed)
 #define EXTRACT_WPAD 8                   // zero window entries on each side of the window table

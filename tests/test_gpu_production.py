@@ -100,8 +100,8 @@ def test_production_12500_per_rank_batch(win):
 
 
 def test_chunked_launch_over_defer_cap():
-    """More clips than one launch may hold (G x EXTRACT_DEFER_CAP = 131 072 on MI355X): the host
-    splits the batch into consecutive launches; clips on both sides of each split match."""
+    """More clips than one launch may hold (G x EXTRACT_DEFER_CAP / 2 = 131 072 on MI355X): the
+    host splits the batch into consecutive launches; clips on both sides of each split match."""
     import torch
     from src.pipeline import FeatureExtractor, create_window
     from src.synth import make_batch_device
