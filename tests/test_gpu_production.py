@@ -1,9 +1,10 @@
 """GPU parity at production batch sizes: the persistent multi-clip loop the benchmark times.
 
-The extraction grid is persistent (two workgroups per CU, 512 on MI355X) and each workgroup walks
-clips i, i + G, i + 2G, ...; these tests launch far more clips than workgroups, so every
-workgroup processes many clips in sequence (LDS summaries reused, near-tie redo list holding
-several clips), and compare everything with the C oracle (reference algorithm:
+The extraction grid is persistent (two workgroups per CU, 512 on MI355X): workgroup w takes clip
+w, then claims clips from a launch-wide queue; these tests launch far more clips than workgroups,
+so every workgroup processes many clips in sequence (LDS summaries reused, the next clip's loads
+issued before R5, near-tie redo list holding several clips), and compare everything with the C
+oracle (reference algorithm:
 src/audio_processing.py:336-396, src/feature_extraction.py:12-88).  They also simulate the
 8-rank sharding of BASELINE configs[3]/[4] on one GPU: shards processed
 separately and concatenated must equal the single launch.
@@ -166,3 +167,35 @@ def test_sharded_knn_self_query_equals_single():
     assert np.array_equal(i_full.cpu().numpy()[lo:hi], i0)
     assert np.array_equal(d_full.cpu().numpy()[lo:hi], d0)
     assert np.array_equal(p_full.cpu().numpy()[lo:hi], p0)
+
+
+def test_small_defer_cap_variant():
+    """The clip queue's claim rule under pressure.  lib/libdsp_audiorec_cap4.so (Makefile) is the
+    product kernel built with a near-tie list of 4 clips per workgroup: a workgroup stops claiming
+    once 3 near ties are listed, and a launch holds G x 4 / 2 clips.  Every third clip of a
+    5G + 37-clip batch is a near tie (3 launches, the last ragged); every clip must be processed,
+    match the oracle, and the near ties must have been redone exactly."""
+    import os
+    import torch
+    from src import _hip
+    from src.pipeline import FeatureExtractor, create_window
+    from src.synth import make_batch
+    G = 2 * torch.cuda.get_device_properties(0).multi_processor_count
+    B = 5 * G + 37
+    base = make_batch(64, base_seed=900)
+    tie = near_tie_clip()
+    clips = [tie if i % 3 == 0 else base[i % 64] for i in range(B)]
+    off = np.zeros(B + 1, np.int64)
+    off[1:] = np.cumsum([c.size for c in clips])
+    pcm = torch.as_tensor(np.concatenate(clips + [np.zeros(8, np.int16)])).cuda()
+    path = os.path.join(os.path.dirname(_hip.LIB_PATH), "libdsp_audiorec_cap4.so")
+    saved = _hip._lib
+    _hip._lib = None
+    try:
+        _hip.load_library(path)
+        fx = FeatureExtractor(L, S, "hamming", True)
+        out = {k: v.cpu().numpy() for k, v in fx(pcm, off).items()}
+    finally:
+        _hip._lib = saved
+    _check(out, clips, create_window("hamming", L))
+    assert ((out["status"][::3] >> 8) & 1).all(), "near ties were not redone exactly"
