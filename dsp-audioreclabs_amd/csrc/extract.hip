@@ -1267,7 +1267,8 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     p.stamps = (unsigned long long *)g_stamp_buffer;
     p.cv = extract_carve((int)max_len, frame_length, frame_shift, EXTRACT_DEFER_CAP);
     // persistent grid: two workgroups per CU when their LDS fits (one otherwise), each walking
-    // clips blockIdx, blockIdx + grid, ...; the compile-time layout whenever the launch fits it
+    // clip blockIdx first, then clips from the launch's queue; the compile-time layout whenever
+    // the launch fits it
     const bool fast = extract_fast_fits((int)max_len, frame_length, frame_shift);
     const size_t lds_launch = fast ? (size_t)extract_carve_fast().total : lds;
     const int per_cu = std::max(1, std::min<int>(EXTRACT_WG_PER_CU, (int)(EXTRACT_LDS_LIMIT / lds_launch)));

@@ -58,7 +58,8 @@ def _check(out, clips, w, vad=True, idx=None):
 
 def test_production_batch_2000_ragged_and_near_ties():
     """2000 clips of BASELINE configs[1] (Hamming, 1102/441, VAD) with empty, short, ragged and
-    near-tie clips scattered; four near-tie clips G apart land in one workgroup's redo list."""
+    near-tie clips scattered; four near-tie clips G apart (round 1's static split put them in one
+    workgroup's redo list; the queue spreads them by claim order)."""
     import torch
     from src.pipeline import FeatureExtractor, create_window
     from src.synth import make_batch
