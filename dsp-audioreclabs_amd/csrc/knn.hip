@@ -709,6 +709,8 @@ KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
     l.mfma = l.exp;  // every expanded-form screen runs on the matrix cores
     l.nsplit = l.mfma ? pick_nsplit_mfma(Nr, Nq, dsp::mq_qpb(l.KC), device_cus())
                       : pick_nsplit(Nr, Nq, l.hd ? dsp::KNN_TQ : dsp::KNN_TQ * dsp::KNN_QP);
+    if (const char *e = getenv("DSP_KNN_NSPLIT"))  // diagnostic sweeps (tools/knn_split_sweep.sh)
+        l.nsplit = std::max(1, std::min(64, atoi(e)));
     size_t o = 0;
     l.ref32 = o; o += al((size_t)Nr * l.DP * 4);
     l.q32 = o;   o += al((size_t)Nq * l.DP * 4);

@@ -1,0 +1,8 @@
+#!/bin/bash
+# KNN reference-split sweep on the GPU box: bench_knn at the given query count for each forced
+# split count (DSP_KNN_NSPLIT) and the model's own pick.  usage: tools/knn_split_sweep.sh Q s1 s2 ...
+cd ${GRAFT_REPO_ROOT:-.}
+Q=$1; shift
+run() { timeout -k 10 120 python3 tools/bench_knn.py --no-cpu --queries $Q | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms'], d['roofline']['frac'])"; }
+echo "Q=$Q model: $(run)"
+for s in "$@"; do echo "Q=$Q nsplit=$s: $(DSP_KNN_NSPLIT=$s run)"; done
