@@ -37,10 +37,6 @@
 #include "extract_layout.h"
 #include "dsp_device.h"
 
-// issue the next clip's loads after R4 (the last phase reading global memory), overlapping R5
-#ifndef EXTRACT_PF_R5
-#define EXTRACT_PF_R5 1
-#endif
 #ifndef EXTRACT_R4_KV
 #define EXTRACT_R4_KV 9
 #endif
@@ -102,8 +98,9 @@ struct ExtractParams {
     float *seq;
     int ld_seq;
     unsigned long long *stamps;  // diagnostic build only (else null)
-    unsigned *queue;             // [0] clips claimed past the first G, [1] workgroups done; both
-                                 // zero at launch, the last workgroup out zeroes them again
+    int queue_slot;              // counter pair g_queue_pool[2 * slot ..]: [0] clips claimed past
+                                 // the first G, [1] workgroups done; both zero at launch, the last
+                                 // workgroup out zeroes them again
     ExtractCarve cv;             // LDS layout, computed on the host (kernel arguments can be
                                  // re-read instead of being held in registers)
 };
@@ -122,6 +119,12 @@ struct Shared {
     int n3, n1, n6, exact, j0, j1, ndefer, next;
 };
 static_assert(sizeof(Shared) <= EXTRACT_SHARED_BYTES, "grow EXTRACT_SHARED_BYTES");
+
+// clip-queue counter pairs, zero-initialised with the code object on each device (no allocation,
+// memset or synchronisation in the entry point); launches take slots round robin on the host, so
+// launches in flight on different streams use different pairs
+static constexpr int QUEUE_SLOTS = 1024;
+__device__ unsigned g_queue_pool[2 * QUEUE_SLOTS];
 
 struct ClipRef {
     int64_t base;  // 8-aligned first sample index of the clip's vectors
@@ -888,10 +891,10 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     }
     if (!FAST && F > 128)
         for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
-    if constexpr (!EXACT && EXTRACT_PF_R5)
+    if constexpr (!EXACT)
         if (tid == 0) sh->next = (int)min(claim, 0x7fffffffu);  // claimed at the clip's start
     __syncthreads();
-    if constexpr (!EXACT && EXTRACT_PF_R5) {
+    if constexpr (!EXACT) {
         // regs are dead since R2: the next clip's words load while R5 runs (unconditional, a
         // clip_none() reads zeros, so the compiler's vmcnt bookkeeping stays exact)
         const int nx = sh->next;
@@ -1138,24 +1141,25 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     // claims only while its near-tie list has room for the current and the claimed clip, and the
     // host keeps a launch at <= G * EXTRACT_DEFER_CAP / 2 clips, so the list never overflows and
     // some workgroup can always claim what is left.
+    unsigned *const queue = g_queue_pool + 2 * p.queue_slot;
     short8 regs[NRV];
-    bool inflight = false;  // regs already hold clip i's loads (EXTRACT_PF_R5)
+    bool inflight = false;  // regs already hold clip i's loads (issued by the previous clip's R4)
     for (int i = blockIdx.x; i < p.B;) {
         const ClipRef cur = clip_ref(p, i);
         unsigned claim = 0x7fffffffu;
         if (!cur.ok) {
             __syncthreads();  // everyone has read sh->next (the ok path has barriers in clip_body)
-            if (tid == 0) claim = (unsigned)G + __hip_atomic_fetch_add(p.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0) claim = (unsigned)G + __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             write_bad_clip(p, i, tid);
             inflight = false;
         } else {
             if (!inflight) issue_clip(regs, p, cur);
             if (tid == 0 && sh->ndefer < EXTRACT_DEFER_CAP - 1)
-                claim = (unsigned)G + __hip_atomic_fetch_add(p.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                claim = (unsigned)G + __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             c.stamp_clip = i;
             const bool done = clip_body<false, FAST>(p, c, i, cur, regs, claim);
             if (!done && tid == 0) c.defer[sh->ndefer++] = i;
-            inflight = EXTRACT_PF_R5 && done;  // a deferred clip returns before R4
+            inflight = done;  // a deferred clip returns before R4
         }
         if (tid == 0) sh->next = (int)min(claim, 0x7fffffffu);
         __syncthreads();  // LDS summaries are rewritten by the next clip; sh->next published
@@ -1172,10 +1176,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     // the last workgroup out resets the queue for the next launch on the stream: every claim of
     // every workgroup precedes its increment of the done count
     if (tid == 0) {
-        const unsigned d = __hip_atomic_fetch_add(p.queue + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned d = __hip_atomic_fetch_add(queue + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         if (d == (unsigned)G - 1) {
-            __hip_atomic_store(p.queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(p.queue + 1, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(queue + 1, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     WG_STAMP(22);
@@ -1200,13 +1204,10 @@ extern "C" size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int f
     return c.total <= EXTRACT_LDS_LIMIT ? (size_t)c.total : 0;
 }
 
-// CU count per device (the persistent grid), cached on first use of each device, and per device
-// a pool of clip-queue counter pairs (ExtractParams::queue): launches take slots round robin, so
-// launches in flight on different streams use different counters
+// CU count per device (the persistent grid), cached on first use of each device; the next
+// clip-queue slot (dsp::g_queue_pool)
 static int g_num_cus[64];
-static constexpr int QUEUE_SLOTS = 1024;
 static_assert(EXTRACT_DEFER_CAP >= 2, "the claim rule keeps room for two clips");
-static unsigned *g_queue[64];
 static std::atomic<unsigned> g_queue_next{0};
 
 extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, int B,
@@ -1231,11 +1232,6 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     if (g_num_cus[dev] == 0) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return DSP_ERR_HIP;
-        unsigned *q = nullptr;
-        if (hipMalloc((void **)&q, sizeof(unsigned) * 2 * QUEUE_SLOTS) != hipSuccess) return DSP_ERR_HIP;
-        if (hipMemset(q, 0, sizeof(unsigned) * 2 * QUEUE_SLOTS) != hipSuccess) return DSP_ERR_HIP;
-        if (hipDeviceSynchronize() != hipSuccess) return DSP_ERR_HIP;
-        g_queue[dev] = q;
         g_num_cus[dev] = prop.multiProcessorCount;
         (void)hipFuncSetAttribute((const void *)dsp::extract_kernel<true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
@@ -1293,7 +1289,7 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
         if (seq) q.seq = seq + b0 * ld_seq * 3;
         if (q.stamps) q.stamps = p.stamps + 32 * b0;
         const int grid = nb < slots ? nb : slots;
-        q.queue = g_queue[dev] + 2 * (g_queue_next.fetch_add(1, std::memory_order_relaxed) % QUEUE_SLOTS);
+        q.queue_slot = (int)(g_queue_next.fetch_add(1, std::memory_order_relaxed) % dsp::QUEUE_SLOTS);
         if (fast)
             hipLaunchKernelGGL(dsp::extract_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch, (hipStream_t)stream, q);
         else
