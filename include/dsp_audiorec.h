@@ -44,8 +44,10 @@ extern "C" {
 #define DSP_CLIP_TOO_LONG 4   /* longer than the max_len given at launch (dsp_extract_general
                                  processes such clips) */
 #define DSP_CLIP_UNCERTIFIED 5 /* reserved: an endpoint decision that could not be certified.
-                                  Never produced: launches are split so that every near tie
-                                  is redone on the exact path */
+                                  Never produced: a workgroup claims clips only while its
+                                  near-tie list has room and launches hold at most
+                                  G x EXTRACT_DEFER_CAP / 2 clips, so every near tie is redone
+                                  on the exact path */
 /* status[b] flag bits (informational) */
 #define DSP_CLIP_FLAG_VAD_EXACT 0x100 /* endpoint decision was a near tie: re-decided on the
                                          bit-exact (numpy-order) fp64 path */
