@@ -235,6 +235,59 @@ __device__ __forceinline__ double np_lerp(double a, double b, double g)
 }
 #pragma clang fp contract(on)
 
+// ---- canonical windowed frame sums (both extraction kernels, so that a clip's features do not
+// depend on where it sits in the packed buffer nor on which kernel ran it) ------------------------
+// A feature frame at clip sample fs with lim real samples (frame_signal :322-331) is summed over
+// the clip's 8-sample vectors v = va .. vb (va = fs >> 3, vb = (fs + lim - 1) >> 3; vector v =
+// clip samples 8v .. 8v + 7) by 16 lanes: lane l takes v = va + l + 16k in increasing k, and each
+// vector's pairs h = 0..3 in order, with j = 8v + 2h (+1) - fs, w = w_j for 0 <= j < lim (else 0),
+//   x = (float)k + xa            (near0: |round(mq)| <= 2; xa = fl(-mq), one rounding of k - mq)
+//   x = ((float)k + xa) + xb     (otherwise: xa = -t0, xb = -(mq - t0); k - t0 exact)
+//   y = w x,  e_t = fma(y_t, y_t, e_t),  m_t = m_t + |y_t|   (t = the pair's first / second sample)
+// Lane value (e_0 + e_1, m_0 + m_1); the frame's sum is dpp_row_reduce over the 16 lanes.
+struct CanonX {
+    float xa, xb;
+    bool near0;
+};
+__device__ __forceinline__ CanonX canon_x(double mq, int t0)
+{
+    CanonX c;
+    c.near0 = t0 >= -2 && t0 <= 2;
+    c.xa = c.near0 ? (float)-mq : (float)-t0;
+    c.xb = c.near0 ? 0.f : -(float)(mq - (double)t0);  // mq - t0 exact (Sterbenz)
+    return c;
+}
+typedef float float2v __attribute__((ext_vector_type(2)));
+#pragma clang fp contract(off)
+__device__ __forceinline__ float canon_xval(int k, const CanonX &c)
+{
+    return c.near0 ? (float)k + c.xa : ((float)k + c.xa) + c.xb;
+}
+// x of a sample pair, packed (v_pk_add_f32): the same bits as canon_xval per sample
+template <bool NEAR0>
+__device__ __forceinline__ float2v canon_x2(int k0, int k1, const CanonX &c)
+{
+    const float2v k = {(float)k0, (float)k1};
+    const float2v a = {c.xa, c.xa}, b = {c.xb, c.xb};
+    return NEAR0 ? k + a : (k + a) + b;
+}
+#pragma clang fp contract(on)
+// one pair: weights w, x values x; y = w x (v_pk_mul_f32), e = fma(y, y, e) (v_pk_fma_f32),
+// m_t += |y_t| (v_add_f32 with the abs source modifier) -- per component exactly the scalar ops
+__device__ __forceinline__ float add_abs_f(float acc, float v)
+{
+    float r;
+    asm("v_add_f32_e64 %0, |%1|, %2" : "=v"(r) : "v"(v), "v"(acc));
+    return r;
+}
+__device__ __forceinline__ void canon_pair(float2v w, float2v x, float2v &e, float &m0, float &m1)
+{
+    const float2v y = w * x;
+    e = __builtin_elementwise_fma(y, y, e);
+    m0 = add_abs_f(m0, y.x);
+    m1 = add_abs_f(m1, y.y);
+}
+
 // acc + |v| in one VOP3 add with the abs source modifier
 __device__ __forceinline__ float add_abs(float acc, float v)
 {

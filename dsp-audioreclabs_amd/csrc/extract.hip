@@ -5,11 +5,12 @@
 //   R1  registers: integer sum / min / max + exact per-word moments (sum k, sum k^2) -> LDS
 //   R2  registers: positive-sample bits per word -> LDS (the ZCR of any range is a popcount)
 //   R3  endpoint detection from the per-word summaries (+ the two partial words of each frame,
-//       re-read from L2), p90 by parallel ranks, double-threshold scan
-//   R4  windowed frames of the crop (samples re-read from L2, window (w, w^2) from LDS)
+//       re-read from L2), p90 by a one-wave bitonic sort, double-threshold scan
+//   R4  windowed frames of the crop (clip-relative vectors re-read from L2, window from LDS)
 //   R5  15-d statistics
-// LDS holds only summaries (~36 KB for 1 s), so a second workgroup on the same CU computes while
-// this one waits for HBM.  Algorithmic traffic: 2 B/sample in + 76 B/clip out.
+// LDS holds only summaries, the window table and the per-frame arrays (~54 KB in the compile-time
+// layout), so a second workgroup on the same CU computes while this one waits for HBM.
+// Algorithmic traffic: 2 B/sample in + 76 B/clip out.
 //
 // Reference functions restated (Hypersonic-cpu/DSP-AudioRecLabs):
 //   preprocess              src/audio_processing.py:78-90
@@ -26,7 +27,9 @@
 //     double-double -> relative error ~1e-16; every threshold decision is certified against a
 //     1e-11 margin and, on a near tie, the clip is redone with the energies in numpy's exact
 //     float64 order (pairwise_sum), so start/end are always the reference's.
-//   * windowed E/M: fp32 on VALU (tolerance 1e-5 rel., measured ~2e-7); statistics in fp64.
+//   * windowed E/M: fp32 on VALU (tolerance 1e-5 rel., measured ~2e-7) in the canonical
+//     clip-coordinate order of dsp_device.h (position independent, = dsp_extract_general);
+//     statistics in fp64.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -184,6 +187,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t clip_rsrc(const ExtractParams 
 __device__ __forceinline__ short8 load_vec(const ExtractParams &p, const ClipRef &c, int v)
 {
     return __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(clip_rsrc(p, c), 16 * v, 0, 0));
+}
+// the clip's own 8-sample vector v (clip samples 8v .. 8v + 7): 2-byte aligned when lead is odd
+__device__ __forceinline__ short8 load_cvec(const ExtractParams &p, const ClipRef &c, int v)
+{
+    return __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(clip_rsrc(p, c), 2 * c.lead + 16 * v, 0, 0));
 }
 __device__ __forceinline__ void issue_word(short8 *q, const ExtractParams &p, const ClipRef &c, int w)
 {
@@ -472,7 +480,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                                           short8 (&regs)[NRV], unsigned claim = 0x7fffffffu)
 {
     Shared *sh = c.sh;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
     const int L = p.L, S = p.S;
     const int n = cur.n, lead = cur.lead, nword = cur.nword;
     float *featb = p.feat + (size_t)i * 15;
@@ -563,8 +571,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     const double Mp = fmax((double)kmax - mq, mq - (double)kmin);
     const int tpos = (int)floor(mq) + 1;
     const int t0 = (int)floor(mq + 0.5);
-    const float deltaf = (float)(mq - (double)t0);  // mq - t0 is exact (Sterbenz)
-    const float invMf = Mp > 0.0 ? __builtin_amdgcn_rcpf((float)Mp) : 0.0f;  // scale only: 1 ulp
+    const float invMf = Mp > 0.0 ? (float)(1.0 / Mp) : 0.0f;  // as dsp_extract_general (same bits)
     const double invM2 = Mp > 0.0 ? 1.0 / (Mp * Mp) : 0.0;  // endpoint energies (one rounding)
     const int nv = (p.do_vad && n >= L) ? (n - L) / S + 1 : 0;
     STAMP(i, 1);
@@ -659,6 +666,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                     }
                 }
                 __syncthreads();
+                STAMP(i, 7);
             }
             // Pass B, one quad per frame: interior word sums and sign changes, each lane a
             // contiguous quarter
@@ -793,51 +801,40 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     STAMP(i, 4);
 
     // ---- R4: windowed frames over the crop [st, en) (:378, :299-333; fe.py:12-43) ---------
-    // wave per frame; the frame's 16-B vectors are re-read from L2 (lane -> vectors va + lane +
-    // 64k); E = sum w^2 x^2, M = sum w |x| with x = (k - t0) - delta, scaled by 1/M' at the end.
+    // One 16-lane row per frame (4 frames per wave), in the canonical order of dsp_device.h: the
+    // frame's clip-relative 8-sample vectors are re-read from L2 (16-B loads at the clip's own
+    // 2-byte alignment) and lane rl takes vectors va + rl + 16k, so the sums do not depend on where
+    // the clip sits in the buffer and equal dsp_extract_general's.  Per sample y = w_j x (the
+    // reference's windowed frame, :329-331), E += y^2, M += |y|; the weights of a vector's 8
+    // samples are two aligned 16-B reads from the window copy shifted by fs mod 4.
     const int m = en - st;  // > 0 always (start < end)
     const int F = (m <= L) ? 1 : (m - L + S - 1) / S + 1;
     const int j0 = sh->j0, j1 = sh->j1;
-    const float t0f = (float)t0;
     const float sE = invMf * invMf, sM = invMf;
-    // Per sample y = w_j * x (the reference's windowed frame, :329-331), E += y^2, M += |y|:
-    // the weights of a vector's 8 samples are two aligned 16-B reads from the window copy
-    // shifted by u0 mod 4; x pairs go through packed fp32 ops.
     const int wrow = EXTRACT_WROW(L);
-    typedef float float2v __attribute__((ext_vector_type(2)));
-    const float2v mt = {-t0f, -t0f}, md = {-deltaf, -deltaf};
-    // |t0| <= 2: x = k - fl(mq) in one packed add (|error| <= 2^-22, i.e. < 1e-6 of any nonzero
-    // |x| of an integer signal); otherwise (k - t0) exactly, then - delta
-    const bool near0 = t0 >= -2 && t0 <= 2;
-    const float2v mqf = {(float)-mq, (float)-mq};
+    const CanonX cx = canon_x(mq, t0);
+    // a 16-B load ending past the clip's last buffer vector drops a dword that straddles the
+    // descriptor's end (range checks are per dword): with an odd lead and a clip ending on a
+    // vector boundary that dword holds the last sample, patched in from the aligned vector
+    const int vfix = ((lead & 1) && ((lead + n) & 7) == 0) ? (n - 1) >> 3 : -1;
+    const short klast = vfix >= 0 ? load_vec(p, cur, cur.nvec - 1)[7] : (short)0;
     auto frame_vec = [&](auto padded_t, auto near_t, const short8 &x8, const float *wr, int jb, int lim,
-                         float2v &ea, float &ma, float &mb) {
+                         float2v &ea, float &m0, float &m1) {
         constexpr bool PADDED = decltype(padded_t)::value, NEAR0 = decltype(near_t)::value;
         const float4 wa = *reinterpret_cast<const float4 *>(wr + jb);
         const float4 wb = *reinterpret_cast<const float4 *>(wr + jb + 4);
         const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
 #pragma unroll
         for (int h = 0; h < 4; h++) {
-            float2v x = {(float)x8[2 * h], (float)x8[2 * h + 1]};
-            if (NEAR0)
-                x = x + mqf;
-            else
-                x = (x + mt) + md;  // (k - t0) exact, then - delta
             float2v w = {wv[2 * h], wv[2 * h + 1]};
             if (PADDED) {  // samples past the crop are zero padding
                 const int j = jb + 2 * h;  // window index of the pair's first sample
                 w.x = j < lim ? w.x : 0.f;
                 w.y = j + 1 < lim ? w.y : 0.f;
             }
-            const float2v y = w * x;
-            ea = y * y + ea;
-            ma = add_abs(ma, y.x);
-            mb = add_abs(mb, y.y);
+            canon_pair(w, canon_x2<NEAR0>(x8[2 * h], x8[2 * h + 1], cx), ea, m0, m1);
         }
     };
-    // one 16-lane row per frame (4 frames per wave): lane rl of the row takes the frame's vectors
-    // va + rl + 16k; every vector load of the frame is issued before any is used, and the row
-    // sums need four DPP steps instead of a wave reduction
     constexpr int R4_KV = EXTRACT_R4_KV;  // vectors per lane in one batch
     const int rl = lane & 15, row = lane >> 4;
     {
@@ -848,32 +845,35 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
             const int fs = st + gc * S;
             const int lim = min(L, en - fs);  // samples beyond the crop are zero padding
             const bool padded = lim < L;
-            const int u0 = lead + fs;
-            const int va = u0 >> 3, vb = (u0 + lim - 1) >> 3;
-            const int r = u0 & 3;  // copy whose rows start at window index = -u0 (mod 4)
+            const int va = fs >> 3, vb = (fs + lim - 1) >> 3;
+            const int r = fs & 3;  // copy whose rows start at window index = -fs (mod 4)
             const float *wr = c.wtab + r * wrow + EXTRACT_WPAD + r;  // wr[j] = w[j], j = -7 .. L + 7
             float2v ea = {0.f, 0.f};
-            float ma = 0.f, mb = 0.f;
+            float m0 = 0.f, m1 = 0.f;
             for (int v0 = va; v0 <= vb; v0 += 16 * R4_KV) {
                 short8 xv[R4_KV];
 #pragma unroll
-                for (int k = 0; k < R4_KV; k++) xv[k] = load_vec(p, cur, v0 + rl + 16 * k);
+                for (int k = 0; k < R4_KV; k++) xv[k] = load_cvec(p, cur, v0 + rl + 16 * k);
+                if (vfix >= 0)  // clip-uniform, rare
+#pragma unroll
+                    for (int k = 0; k < R4_KV; k++)
+                        if (v0 + rl + 16 * k == vfix) xv[k][(n - 1) & 7] = klast;
                 auto run = [&](auto pt, auto nt) {
 #pragma unroll
                     for (int k = 0; k < R4_KV; k++) {
                         const int v = v0 + rl + 16 * k;
-                        if (v <= vb) frame_vec(pt, nt, xv[k], wr, 8 * v - u0, lim, ea, ma, mb);
+                        if (v <= vb) frame_vec(pt, nt, xv[k], wr, 8 * v - fs, lim, ea, m0, m1);
                     }
                 };
                 if (padded)
-                    run(BoolT<true>(), BoolT<false>());
-                else if (near0)
+                    cx.near0 ? run(BoolT<true>(), BoolT<true>()) : run(BoolT<true>(), BoolT<false>());
+                else if (cx.near0)
                     run(BoolT<false>(), BoolT<true>());
                 else
                     run(BoolT<false>(), BoolT<false>());
             }
             const float E1 = dpp_row_reduce(ea.x + ea.y, OpAdd()) * sE;
-            const float M1 = dpp_row_reduce(ma + mb, OpAdd()) * sM;
+            const float M1 = dpp_row_reduce(m0 + m1, OpAdd()) * sM;
             // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in
             // [j0, j1]) and j < lim; transitions into the window's zero ends / padding count too
             const int ia = fs + j0, ib = min(fs + j1, en - 1);  // sample coords
@@ -889,6 +889,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
             }
         }
     }
+    STAMP(i, 12);
     if (!FAST && F > 128)
         for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
     if constexpr (!EXACT)
@@ -1088,7 +1089,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     float *wt = const_cast<float *>(c.wtab);
     Shared *sh = c.sh;
 
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int L = p.L, G = gridDim.x;
     WG_STAMP(16);
 

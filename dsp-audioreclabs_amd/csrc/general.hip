@@ -11,7 +11,8 @@
 //   * endpoint energies from exact integer moments in float64, every threshold decision
 //     certified against a 1e-11 margin, near ties redone in numpy's pairwise float64 order;
 //   * positive samples k >= floor(mq) + 1 (integer), every ZCR exact;
-//   * windowed E / M in fp32 per lane, reduced in fp64; statistics in fp64.
+//   * windowed E / M in fp32 in the canonical order of dsp_device.h (the fused kernel's bits);
+//     statistics in fp64.
 // Reference functions restated: preprocess :78-90, endpoint_detection :135-275, frame_signal
 // :299-333, extract_frame_features fe.py:12-43, compute_statistics fe.py:46-62.
 #include <hip/hip_runtime.h>
@@ -206,7 +207,7 @@ template <typename T>
 __global__ __launch_bounds__(NT) void general_kernel(Params p)
 {
     __shared__ Sh s;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int i = p.index ? p.index[blockIdx.x] : (int)blockIdx.x;
     const int64_t o0 = p.offsets[i], nn = p.offsets[i + 1] - o0;
     if (nn <= 0 && p.min_len == 0) {  // np.max of an empty array raises (:72)
@@ -382,35 +383,42 @@ __global__ __launch_bounds__(NT) void general_kernel(Params p)
             }
     }
 
-    // ---- windowed frames of the crop [st, en) (:378, :299-333; fe.py:12-43): wave per frame --
-    // frame g covers crop samples [g S, g S + L), zero-padded past the crop; x = (k - t0) - delta
-    const float dlt = (float)delta;
-    for (int64_t gi = wid; gi < F; gi += NWAVE) {
-        const int64_t fs = st + gi * S;
+    // ---- windowed frames of the crop [st, en) (:378, :299-333; fe.py:12-43) ---------------
+    // frame g covers crop samples [g S, g S + L), zero-padded past the crop.  One 16-lane row per
+    // frame, E / M in the canonical order of dsp_device.h (the fused kernel's, same bits); the
+    // ZCR is exact either way.
+    const CanonX cx = canon_x(mq, t0);
+    const int rl = lane & 15, row = lane >> 4;
+    for (int64_t gi = wid; 4 * gi < F; gi += NWAVE) {
+        const int64_t g = 4 * gi + row;
+        const bool act = g < F;
+        const int64_t fs = st + (act ? g : F - 1) * S;
         const int64_t lim = min((int64_t)L, en - fs);
-        float e = 0.f, m = 0.f;
-        int zc = 0;
-        for (int j = lane; j < L; j += 64) {
-            const double wj = p.window[j];
-            const bool in = j < lim;
-            const int k = in ? sample(x, fs + j) : 0;
-            const float xv = in ? (float)(k - t0) - dlt : 0.f;
-            const float y = (float)wj * xv;
-            e = fmaf(y, y, e);
-            m += fabsf(y);
-            if (j + 1 < L) {
-                const bool p0 = in && wj > 0.0 && k >= tpos;
-                const bool in1 = j + 1 < lim;
-                const bool p1 = in1 && p.window[j + 1] > 0.0 && sample(x, fs + j + 1) >= tpos;
-                zc += p0 != p1;
+        const int64_t va = fs >> 3, vb = (fs + lim - 1) >> 3;
+        float2v ea = {0.f, 0.f};
+        float m0 = 0.f, m1 = 0.f;
+        for (int64_t v = va + rl; v <= vb; v += 16)
+            for (int h = 0; h < 4; h++) {
+                float2v wv, xv;
+                for (int t = 0; t < 2; t++) {
+                    const int64_t sj = 8 * v + 2 * h + t, j = sj - fs;
+                    wv[t] = (j >= 0 && j < lim) ? (float)p.window[j] : 0.f;
+                    xv[t] = sj < n ? canon_xval(sample(x, sj), cx) : 0.f;
+                }
+                canon_pair(wv, xv, ea, m0, m1);
             }
+        const float es = dpp_row_reduce(ea.x + ea.y, OpAdd()), ms = dpp_row_reduce(m0 + m1, OpAdd());
+        int zc = 0;
+        for (int j = rl; j + 1 < L; j += 16) {
+            const bool p0 = j < lim && p.window[j] > 0.0 && sample(x, fs + j) >= tpos;
+            const bool p1 = j + 1 < lim && p.window[j + 1] > 0.0 && sample(x, fs + j + 1) >= tpos;
+            zc += p0 != p1;
         }
-        const double es = wave_sum((double)e), ms = wave_sum((double)m);
-        zc = wave_sum(zc);
-        if (lane == 0) {
-            w.fE[gi] = (float)es * (invMf * invMf);
-            w.fM[gi] = (float)ms * invMf;
-            w.fZ[gi] = zc;
+        zc = dpp_row_reduce(zc, OpAdd());
+        if (act && rl == 0) {
+            w.fE[g] = es * (invMf * invMf);
+            w.fM[g] = ms * invMf;
+            w.fZ[g] = zc;
         }
     }
     __syncthreads();

@@ -83,12 +83,14 @@ def _general(pcm, off, L, S, win, vad=True, sample_bytes=2, nv_ld=None):
                status=torch.empty(B, dtype=torch.int32, device=d),
                vad_energy=torch.zeros((B, ld), dtype=torch.float64, device=d),
                vad_zcr=torch.zeros((B, ld), dtype=torch.int32, device=d))
+    ldf = 1 if ml <= L else (ml - L + S - 1) // S + 1
+    out["seq"] = torch.zeros((B, ldf, 3), dtype=torch.float32, device=d)
     nb = lib.dsp_extract_general_workspace_bytes(B, ml, L, S)
     ws = torch.empty(nb, dtype=torch.uint8, device=d)
     P = _hip.ptr
     rc = lib.dsp_extract_general(P(t), sample_bytes, P(o), None, B, 0, ml, L, S, P(w), int(vad), 0.5, 0.1, 1.5,
                                  P(out["feat"]), P(out["start_end"]), P(out["n_frames"]), P(out["status"]),
-                                 P(out["vad_energy"]), P(out["vad_zcr"]), ld, None, 0, P(ws), nb,
+                                 P(out["vad_energy"]), P(out["vad_zcr"]), ld, P(out["seq"]), ldf, P(ws), nb,
                                  _hip.stream_handle(d))
     _hip.check(rc, "dsp_extract_general")
     return {k: v.cpu().numpy() for k, v in out.items()}

@@ -1,0 +1,113 @@
+"""Per-clip results do not depend on where a clip sits in the packed buffer, nor on which kernel
+processed it.  Both extraction kernels sum the windowed frames in one canonical order defined in
+clip coordinates (csrc/dsp_device.h), so:
+  * the same clips packed at leads 0..7 (every alignment of a clip's first sample to the 16-B
+    vectors of the buffer) give bit-identical feat / seq / start_end / n_frames / status;
+  * dsp_extract_general (global-memory kernel) and dsp_extract_features (fused) give the same bits;
+  * extraction over shard_range blocks concatenates to the single launch for any shard size
+    (gather(shards) == single-GPU output), e.g. B = 6001 over 8 ranks.
+The reference computes per file (experiments/run_experiments.py:82-111): a clip's features are a
+function of the clip alone.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from test_gpu_extract import feat_close
+
+pytestmark = pytest.mark.gpu
+
+L, S = 1102, 441
+
+
+def _clips():
+    """1 s clips plus lengths that end on / off vector boundaries at every lead (the odd-lead
+    clip whose last sample sits in a straddling dword), short and padded-tail clips."""
+    from src.synth import make_clip
+    lens = [44100, 44100, 44099, 44097, 40001, 30007, 22050, 8191, 5000, 1500, 1103, 1102, 700, 44095,
+            44093, 44091, 44089, 12345, 20001, 44100 - 3]
+    return [make_clip(7000 + i, n) for i, n in enumerate(lens)]
+
+
+def _pack(clips, lead):
+    """Pack clips back to back after `lead` junk samples: every clip moves by `lead` samples."""
+    parts = [np.full(lead, 1234, np.int16)] + list(clips) + [np.zeros(16, np.int16)]
+    off = np.zeros(len(clips) + 1, np.int64)
+    off[0] = lead
+    off[1:] = lead + np.cumsum([len(c) for c in clips])
+    return np.concatenate(parts), off
+
+
+def _run(fx, pcm, off):
+    import torch
+    o = fx(torch.as_tensor(pcm).cuda(), off)
+    return {k: v.cpu().numpy().copy() for k, v in o.items()}
+
+
+@pytest.mark.parametrize("win,vad", [("hamming", True), ("hanning", False), ("rectangular", True)])
+def test_leads_bit_identical(win, vad):
+    from src.pipeline import FeatureExtractor
+    clips = _clips()
+    fx = FeatureExtractor(L, S, win, vad, return_sequences=True, return_vad_lists=True)
+    base = None
+    for lead in range(8):
+        pcm, off = _pack(clips, lead)
+        out = _run(fx, pcm, off)
+        assert not (out["status"] & 0xFF).any()
+        if base is None:
+            base = out
+            from src.pipeline import create_window
+            w = create_window(win, L)
+            for i, c in enumerate(clips):  # and the oracle, once
+                r = oracle.process_clip(c, L, S, w, do_vad=vad)
+                assert tuple(out["start_end"][i]) == (r["start"], r["end"]), i
+                assert not feat_close(out["feat"][i], r["feat"]).any(), i
+            continue
+        for k in base:
+            assert np.array_equal(base[k], out[k]), (lead, k)
+
+
+def test_general_equals_fused_bitwise():
+    """dsp_extract_general on clips the fused kernel also takes: the same bits."""
+    from src.pipeline import FeatureExtractor
+    from test_gpu_general import _general
+    clips = _clips()
+    pcm, off = _pack(clips, 3)
+    for win, vad in (("hamming", True), ("hanning", True), ("rectangular", False)):
+        fx = FeatureExtractor(L, S, win, vad, return_sequences=True)
+        a = _run(fx, pcm, off)
+        b = _general(pcm, off, L, S, win, vad)
+        for k in ("feat", "start_end", "n_frames", "status"):
+            assert np.array_equal(a[k], b[k]), (win, vad, k)
+        F = a["n_frames"]
+        for i in range(len(clips)):
+            assert np.array_equal(a["seq"][i, :F[i]], b["seq"][i, :F[i]]), (win, vad, i)
+
+
+def test_sharded_extraction_odd_shard_size():
+    """8 simulated ranks over B = 6001 clips (blocks of 751 / 750: every rank after the first
+    starts at a different lead): the concatenation equals the single launch bit for bit."""
+    import torch
+    from src.distributed import shard_range
+    from src.pipeline import FeatureExtractor
+    from src.synth import make_batch_device
+    B, P = 6001, 8
+    x = make_batch_device(B, "cuda", base_seed=21)
+    flat = x.reshape(-1)
+    off = torch.arange(B + 1, dtype=torch.int64, device="cuda") * x.shape[1]
+    fx = FeatureExtractor(L, S, "hamming", True)
+    full = {k: v.clone() for k, v in fx(flat, off).items()}
+    parts = []
+    for r in range(P):
+        lo, hi = shard_range(B, r, P)
+        # each rank packs only its block: the block's first clip lands at the rank's own lead
+        sub = flat[lo * x.shape[1]:hi * x.shape[1]].clone()
+        o = torch.arange(hi - lo + 1, dtype=torch.int64, device="cuda") * x.shape[1]
+        parts.append({k: v.clone() for k, v in fx(sub, o).items()})
+    for k in full:
+        assert torch.equal(torch.cat([p_[k] for p_ in parts]), full[k]), k
+    # and a shifted copy of the whole batch (lead 5): same bits
+    shifted = torch.cat([torch.zeros(5, dtype=torch.int16, device="cuda"), flat, torch.zeros(8, dtype=torch.int16, device="cuda")])
+    sh = fx(shifted, off + 5)
+    for k in full:
+        assert torch.equal(sh[k], full[k]), k

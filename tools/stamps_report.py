@@ -19,8 +19,8 @@ print("clip us  p50 %.2f p90 %.2f | first round p50 %.2f (wg<%d %.2f, wg>=%d %.2
     np.median(tot), np.percentile(tot, 90), np.median(tot[:G]), G // 2, np.median(tot[:G // 2]), G // 2,
     np.median(tot[G // 2:G]), np.median(tot[G:]) if C > G else 0))
 names = {1: "R1 load+stats", 2: "R2 pos", 7: "VAD pass A", 8: "VAD pass B", 3: "p90", 10: "noise+thr", 11: "scan",
-         4: "vad out", 5: "R4", 9: "R5 medians", 6: "R5 stats"}
-seq = [0, 1, 2, 7, 8, 3, 10, 11, 4, 5, 9, 6]
+         4: "vad out", 12: "R4 frames", 5: "R4 barrier+issue", 9: "R5 jobs", 6: "R5 out"}
+seq = [0, 1, 2, 7, 8, 3, 10, 11, 4, 12, 5, 9, 6]
 for a, b in zip(seq, seq[1:]):
     d = (st[:, b] - st[:, a]) / cyc
     print("  %-14s p50 %.2f  oldWG %.2f newWG %.2f" % (names[b], np.median(d), np.median(d[:G // 2]), np.median(d[G // 2:G])))
