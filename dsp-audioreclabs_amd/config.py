@@ -21,6 +21,12 @@ FRAME_LENGTH_MS = 25
 FRAME_SHIFT_MS = 10
 FRAME_LENGTH = int(SAMPLE_RATE * FRAME_LENGTH_MS / 1000)   # 1102
 FRAME_SHIFT = int(SAMPLE_RATE * FRAME_SHIFT_MS / 1000)     # 441
+# Frame sizes in samples, overriding the ms values above: BASELINE.json configs[0] quotes the
+# reference's CPU run at 1024 / 512 samples, which no integer-ms setting of config.py:35-40 gives
+# (int(44100 * ms / 1000)).  Environment DSP_FRAME_LENGTH / DSP_FRAME_SHIFT, or
+# run.py --frame-length / --frame-shift.
+FRAME_LENGTH = int(os.environ.get('DSP_FRAME_LENGTH', FRAME_LENGTH))
+FRAME_SHIFT = int(os.environ.get('DSP_FRAME_SHIFT', FRAME_SHIFT))
 
 # endpoint detection (config.py:43-45)
 ENERGY_HIGH_RATIO = 0.5

@@ -203,12 +203,11 @@ __device__ unsigned long long radix_select(Sh &s, const unsigned long long *key,
     return prefix;
 }
 
+// one clip (number i), start to finish, by the whole workgroup; w is the workgroup's workspace
 template <typename T>
-__global__ __launch_bounds__(NT) void general_kernel(Params p)
+__device__ __forceinline__ void general_clip(const Params &p, Sh &s, const Ws &w, int i)
 {
-    __shared__ Sh s;
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int i = p.index ? p.index[blockIdx.x] : (int)blockIdx.x;
     const int64_t o0 = p.offsets[i], nn = p.offsets[i + 1] - o0;
     if (nn <= 0 && p.min_len == 0) {  // np.max of an empty array raises (:72)
         if (tid < 15) p.feat[(int64_t)i * 15 + tid] = __builtin_nanf("");
@@ -223,7 +222,6 @@ __global__ __launch_bounds__(NT) void general_kernel(Params p)
     const T *x = reinterpret_cast<const T *>(p.pcm) + o0;
     const int64_t n = nn;
     const int L = p.L, S = p.S;
-    const Ws w = ws_at(p, blockIdx.x);
 
     // ---- preprocess (:49-75): exact integer sum / min / max ---------------------------------
     long long ks = 0;
@@ -475,6 +473,21 @@ __global__ __launch_bounds__(NT) void general_kernel(Params p)
     }
 }
 
+// Persistent grid: workgroup b takes list entries b, b + G, ... and keeps its workspace slot b,
+// so the workspace is min(nclip, GEN_GRID) slots and a launch over a whole batch (clip_index
+// NULL, the length window selecting the clips) needs no host-side selection.
+constexpr int GEN_GRID = 1024;
+template <typename T>
+__global__ __launch_bounds__(NT) void general_kernel(Params p)
+{
+    __shared__ Sh s;
+    const Ws w = ws_at(p, blockIdx.x);
+    for (int j = blockIdx.x; j < p.nclip; j += gridDim.x) {
+        general_clip<T>(p, s, w, p.index ? p.index[j] : j);
+        __syncthreads();  // shared state and the workspace slot are the next clip's
+    }
+}
+
 }  // namespace gen
 }  // namespace dsp
 
@@ -484,7 +497,7 @@ extern "C" size_t dsp_extract_general_workspace_bytes(int64_t nclip, int64_t max
     if (nclip < 1 || max_len < 1 || frame_length < 1 || frame_shift < 1) return 0;
     const int64_t nv = max_len >= frame_length ? (max_len - frame_length) / frame_shift + 1 : 1;
     const int64_t F = max_len <= frame_length ? 1 : (max_len - frame_length + frame_shift - 1) / frame_shift + 1;
-    return (size_t)(nclip * dsp::gen::ws_stride(nv, F));
+    return (size_t)(std::min<int64_t>(nclip, dsp::gen::GEN_GRID) * dsp::gen::ws_stride(nv, F));
 }
 
 extern "C" int dsp_extract_general(const void *pcm, int sample_bytes, const int64_t *offsets,
@@ -533,10 +546,11 @@ extern "C" int dsp_extract_general(const void *pcm, int sample_bytes, const int6
     p.nvcap = max_len >= frame_length ? (max_len - frame_length) / frame_shift + 1 : 1;
     p.fcap = max_len <= frame_length ? 1 : (max_len - frame_length + frame_shift - 1) / frame_shift + 1;
     p.ws_stride = dsp::gen::ws_stride(p.nvcap, p.fcap);
+    const unsigned grid = (unsigned)std::min(nclip, dsp::gen::GEN_GRID);
     if (sample_bytes == 2)
-        hipLaunchKernelGGL(dsp::gen::general_kernel<int16_t>, dim3(nclip), dim3(dsp::gen::NT), 0, (hipStream_t)stream, p);
+        hipLaunchKernelGGL(dsp::gen::general_kernel<int16_t>, dim3(grid), dim3(dsp::gen::NT), 0, (hipStream_t)stream, p);
     else
-        hipLaunchKernelGGL(dsp::gen::general_kernel<int32_t>, dim3(nclip), dim3(dsp::gen::NT), 0, (hipStream_t)stream, p);
+        hipLaunchKernelGGL(dsp::gen::general_kernel<int32_t>, dim3(grid), dim3(dsp::gen::NT), 0, (hipStream_t)stream, p);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? DSP_OK : DSP_ERR_HIP + (int)e;
 }

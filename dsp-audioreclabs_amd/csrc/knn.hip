@@ -671,10 +671,14 @@ int pick_nsplit(int64_t Nr, int64_t Nq, int qpb)
     // Enough workgroups to fill the chip (two per CU), as few reference splits as that allows:
     // a longer split makes a screened distance that enters its top list rarer (~KC / rows seen),
     // and a wave pays for an insertion whenever any of its 64 lanes makes one
+#ifdef DSP_KNN_DIAG  // diagnostic build only (tools/knn_split_sweep.sh): launch-shape override
     static const int target = [] {
         const char *e = getenv("DSP_KNN_TARGET_WGS");
         return e ? atoi(e) : 512;
     }();
+#else
+    constexpr int target = 512;
+#endif
     int64_t s = (target + qblocks - 1) / qblocks;
     const int64_t maxs = (Nr + dsp::KNN_TR - 1) / dsp::KNN_TR;  // >= one tile per split
     if (s > maxs) s = maxs;
@@ -709,8 +713,9 @@ KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
     l.mfma = l.exp;  // every expanded-form screen runs on the matrix cores
     l.nsplit = l.mfma ? pick_nsplit_mfma(Nr, Nq, dsp::mq_qpb(l.KC), device_cus())
                       : pick_nsplit(Nr, Nq, l.hd ? dsp::KNN_TQ : dsp::KNN_TQ * dsp::KNN_QP);
-    if (const char *e = getenv("DSP_KNN_NSPLIT"))  // diagnostic sweeps (tools/knn_split_sweep.sh)
-        l.nsplit = std::max(1, std::min(64, atoi(e)));
+#ifdef DSP_KNN_DIAG  // diagnostic build only: forced split count (tools/knn_split_sweep.sh)
+    if (const char *e = getenv("DSP_KNN_NSPLIT")) l.nsplit = std::max(1, std::min(64, atoi(e)));
+#endif
     size_t o = 0;
     l.ref32 = o; o += al((size_t)Nr * l.DP * 4);
     l.q32 = o;   o += al((size_t)Nq * l.DP * 4);

@@ -11,6 +11,8 @@ import argparse
 import os
 import sys
 
+last_experiment = None
+
 
 def main(argv=None):
     ap = argparse.ArgumentParser(description="isolated-word recognition experiments (MI355X)")
@@ -19,18 +21,31 @@ def main(argv=None):
     ap.add_argument('--experiment', type=str, default='all',
                     choices=['all', 'classifier', 'window', 'feature', 'visualize'])
     ap.add_argument('--window-type', type=str, default='hamming', choices=['rectangular', 'hamming', 'hanning'])
+    # frame sizes in samples (config.FRAME_LENGTH / FRAME_SHIFT; BASELINE configs[0]: 1024 / 512)
+    ap.add_argument('--frame-length', type=int, default=None, help='frame length in samples')
+    ap.add_argument('--frame-shift', type=int, default=None, help='frame shift in samples')
     args = ap.parse_args(argv)
     if args.data_dir:
         os.environ['SPEECH_DATA_DIR'] = os.path.abspath(os.path.expanduser(args.data_dir))
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import config
     from experiments.run_experiments import SpeechRecognitionExperiment
+    global last_experiment
+    if args.frame_length is not None:
+        if args.frame_length < 1:
+            ap.error('--frame-length must be positive')
+        config.FRAME_LENGTH = args.frame_length
+    if args.frame_shift is not None:
+        if args.frame_shift < 1:
+            ap.error('--frame-shift must be positive')
+        config.FRAME_SHIFT = args.frame_shift
     data_dir = os.environ.get('SPEECH_DATA_DIR', config.DATA_DIR)
     if not os.path.isdir(data_dir):
         print("data directory not found: %s (use --data-dir)" % data_dir)
         return 1
     exp = SpeechRecognitionExperiment(data_dir, args.results_dir or config.RESULTS_DIR)
-    out = {}
+    last_experiment = exp  # the last run's data (X, y), for callers that drive main() in process
+    out = {'frame_length': config.FRAME_LENGTH, 'frame_shift': config.FRAME_SHIFT}
     if args.experiment in ('all', 'classifier'):
         res = exp.experiment_classifier_comparison(window_type=args.window_type)
         out['classifier'] = {k: float(v['accuracy']) for k, v in res.items()}

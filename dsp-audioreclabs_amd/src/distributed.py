@@ -8,6 +8,8 @@ CPU in the tests.  Block sizes follow from ``shard_range`` on every rank, so no 
 and no host sync precede the collective.  KNN then shards the queries and gathers the per-query
 results (idx, dist, pred) the same way, again as one collective.
 """
+import math
+
 import torch
 import torch.distributed as dist
 
@@ -35,7 +37,9 @@ def _pack_rows(tensors, rows):
     for name, t in tensors.items():
         if t.shape[0] != rows:
             raise ValueError("%s has %d rows, expected %d" % (name, t.shape[0], rows))
-        b = t.contiguous().reshape(rows, -1).view(torch.uint8)
+        # explicit column count: an empty block (total < world size) still packs as [0, row_bytes]
+        # and reaches the collective with the other ranks
+        b = t.contiguous().reshape(rows, math.prod(t.shape[1:])).view(torch.uint8)
         layout.append((name, t.dtype, tuple(t.shape[1:]), b.shape[1]))
         cols.append(b)
     return torch.cat(cols, dim=1) if cols else None, layout
@@ -45,7 +49,9 @@ def _unpack_rows(packed, layout):
     out, c = {}, 0
     n = packed.shape[0]
     for name, dtype, tail, nb in layout:
-        out[name] = packed[:, c:c + nb].contiguous().view(dtype).reshape((n,) + tail)
+        # clone, not contiguous(): a one-row slice is already "contiguous" at a byte offset that
+        # need not be a multiple of the element size, and view(dtype) needs an aligned offset
+        out[name] = packed[:, c:c + nb].clone().view(dtype).reshape((n,) + tail)
         c += nb
     return out
 

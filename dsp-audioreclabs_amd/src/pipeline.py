@@ -95,15 +95,16 @@ class FeatureExtractor:
         int16 clips that fit the fused kernel's on-chip plan run in one fused launch; longer
         clips, and int32 samples (16-bit stereo channel sums), run on dsp_extract_general in the
         same stream order.  An explicit ``max_len`` caps the clips processed (longer ones report
-        DSP_CLIP_TOO_LONG).  Returns a dict of device tensors: feat [B,15] f32, start_end [B,2]
-        i32, n_frames [B] i32, status [B] i32 (+ vad_energy/vad_zcr, seq when requested).  The
-        tensors are reused by the next call with the same shape.
+        DSP_CLIP_TOO_LONG); without it, device-tensor offsets cost one host sync (the longest
+        clip sizes the launch), so pass ``max_len`` to capture the call in a HIP graph.  Returns a
+        dict of device tensors: feat [B,15] f32, start_end [B,2] i32, n_frames [B] i32, status
+        [B] i32 (+ vad_energy/vad_zcr, seq when requested).  The tensors are reused by the next
+        call with the same shape.
         """
         import torch
         d = self.device
         wide = str(getattr(pcm, "dtype", "")) in ("int32", "torch.int32")
         pcm = _as_device(pcm, torch.int32 if wide else torch.int16, d)
-        lens = None  # host clip lengths, when known without a device round trip
         if offsets is None:
             if pcm.dim() != 2:
                 raise ValueError("1-D packed pcm needs offsets")
@@ -113,7 +114,6 @@ class FeatureExtractor:
                 self._bufs[key] = torch.arange(B + 1, dtype=torch.int64, device=d) * N
             off = self._bufs[key]
             true_max = N
-            lens = np.full(B, N, dtype=np.int64)
         else:
             if isinstance(offsets, np.ndarray) or not isinstance(offsets, torch.Tensor):
                 lens = np.diff(np.asarray(offsets, dtype=np.int64))
@@ -140,26 +140,23 @@ class FeatureExtractor:
                 _hip.ptr(out["n_frames"]), _hip.ptr(out["status"]), _hip.ptr(ve), _hip.ptr(vz), ldv,
                 _hip.ptr(sq), lds_)
         cap = 0 if wide else self.fused_cap()
-        if not wide and B > 0:
+        if not wide and B > 0 and cap > 0:
             rc = _hip.lib().dsp_extract_features(
-                _hip.ptr(pcm), _hip.ptr(off), B, min(max_len, cap) if cap > 0 else max_len, self.L, self.S,
+                _hip.ptr(pcm), _hip.ptr(off), B, min(max_len, cap), self.L, self.S,
                 _hip.ptr(self.window), *args, _hip.stream_handle(d))
             _hip.check(rc, "dsp_extract_features")
         if B > 0 and (wide or max_len > cap):
-            # the clips the fused kernel cannot hold: one workgroup each, from global memory
-            if lens is None:
-                lens = (off[1:] - off[:-1]).cpu().numpy()
-            sel = np.nonzero((lens > cap) & (lens <= max_len) | (wide & (lens <= 0)))[0].astype(np.int32)
-            if sel.size:
-                idx = torch.as_tensor(sel).to(d)
-                nbytes = _hip.lib().dsp_extract_general_workspace_bytes(sel.size, max_len, self.L, self.S)
-                ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=d)
-                rc = _hip.lib().dsp_extract_general(
-                    _hip.ptr(pcm), 4 if wide else 2, _hip.ptr(off), _hip.ptr(idx), int(sel.size),
-                    0 if wide else cap, max_len, self.L, self.S, _hip.ptr(self.window), *args,
-                    _hip.ptr(ws), nbytes, _hip.stream_handle(d))
-                _hip.check(rc, "dsp_extract_general")
-                self._keep = (idx, ws)  # alive until the next call (stream-ordered use)
+            # the clips the fused kernel cannot hold (longer than cap, or every clip of an int32
+            # batch, or all of them when the fused plan holds none at this frame length): the
+            # general kernel over the whole batch, its length window [cap + 1, max_len] selecting
+            # them on the device -- no host round trip, so the call stays graph-capturable
+            nbytes = _hip.lib().dsp_extract_general_workspace_bytes(B, max_len, self.L, self.S)
+            ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=d)
+            rc = _hip.lib().dsp_extract_general(
+                _hip.ptr(pcm), 4 if wide else 2, _hip.ptr(off), None, B, cap, max_len, self.L, self.S,
+                _hip.ptr(self.window), *args, _hip.ptr(ws), nbytes, _hip.stream_handle(d))
+            _hip.check(rc, "dsp_extract_general")
+            self._keep = ws  # stream-ordered use: the caching allocator reuses it only after the launch
         return out
 
 

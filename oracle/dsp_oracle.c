@@ -59,6 +59,13 @@ static double *ws_alloc(size_t n_doubles)
     return p;
 }
 static void ws_free(size_t n_doubles) { tl_top -= ws_round(n_doubles * sizeof(double) + 8); }
+/* a worker thread's arena dies with it (found by the ASan build, oracle/asan_check.c) */
+static void ws_release(void)
+{
+    free(tl_buf);
+    tl_buf = NULL;
+    tl_cap = tl_top = 0;
+}
 static size_t ws_bound(int64_t n, int64_t L, int64_t S)
 {
     int64_t nf = n / (S > 0 ? S : 1) + 4;
@@ -418,6 +425,7 @@ typedef struct {
     double *feat;
     int64_t *start_end, *n_frames;
     int32_t *status;
+    int own_thread; /* runs on a thread of its own: release the arena at the end */
 } batch_job;
 
 static void *batch_worker(void *arg)
@@ -430,6 +438,7 @@ static void *batch_worker(void *arg)
                                      j->n_frames + b, NULL, NULL, NULL, NULL, 0);
         j->status[b] = rc;
     }
+    if (j->own_thread) ws_release();
     return NULL;
 }
 
@@ -445,7 +454,7 @@ int ora_process_batch_i16(const int16_t *pcm, const int64_t *offsets, int64_t B,
     batch_job *jobs = (batch_job *)malloc(sizeof(batch_job) * (size_t)nthreads);
     for (int t = 0; t < nthreads; t++) {
         batch_job j = {pcm, offsets, B * t / nthreads, B * (t + 1) / nthreads, L, S, window,
-                       do_vad, hi, lo, zr, feat, start_end, n_frames, status};
+                       do_vad, hi, lo, zr, feat, start_end, n_frames, status, nthreads > 1};
         jobs[t] = j;
         if (nthreads == 1)
             batch_worker(&jobs[t]);

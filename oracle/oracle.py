@@ -153,7 +153,10 @@ def zscore_fit(X):
     return mean, std
 
 
-def knn(ref, ref_labels, query, k, n_classes=None, self_offset=-1):
+def knn(ref, ref_labels, query, k, n_classes=None, self_offset=-1, nthreads=1):
+    """sklearn KNeighborsClassifier(k) kneighbors + predict, restated (dsp_oracle.c ora_knn).
+    With nthreads > 1 the queries are split into contiguous blocks answered on that many host
+    threads (ctypes releases the GIL); self_offset follows each block."""
     ref = np.ascontiguousarray(ref, dtype=np.float64)
     q = np.ascontiguousarray(query, dtype=np.float64)
     lbl = np.ascontiguousarray(ref_labels, dtype=np.int32)
@@ -164,6 +167,21 @@ def knn(ref, ref_labels, query, k, n_classes=None, self_offset=-1):
     idx = np.zeros((Nq, k), np.int32)
     dist = np.zeros((Nq, k))
     pred = np.zeros(Nq, np.int32)
-    lib().ora_knn(_p(ref, _D), _p(lbl, _I32), Nr, _p(q, _D), Nq, D, k, self_offset, n_classes,
-                  _p(idx, _I32), _p(dist, _D), _p(pred, _I32))
+    L = lib()
+
+    def run(a, b):
+        if b <= a:
+            return
+        L.ora_knn(_p(ref, _D), _p(lbl, _I32), Nr, _p(q[a:b], _D), b - a, D, k,
+                  self_offset + a if self_offset >= 0 else -1, n_classes,
+                  _p(idx[a:b], _I32), _p(dist[a:b], _D), _p(pred[a:b], _I32))
+
+    nthreads = max(1, min(int(nthreads), Nq))
+    if nthreads == 1:
+        run(0, Nq)
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+        cuts = [Nq * t // nthreads for t in range(nthreads + 1)]
+        with ThreadPoolExecutor(nthreads) as ex:
+            list(ex.map(lambda t: run(cuts[t], cuts[t + 1]), range(nthreads)))
     return idx, dist, pred

@@ -39,6 +39,10 @@ def _worker(rank, ws, port, out_dir):
 
         def extract(pcm):
             n, N = pcm.shape
+            if n == 0:  # this rank's block is empty (total < world size)
+                return {"feat": torch.zeros((0, 15), dtype=torch.float64),  # the oracle's dtypes
+                        "start_end": torch.zeros((0, 2), dtype=torch.int64),
+                        "n_frames": torch.zeros(0, dtype=torch.int64)}
             r = oracle.process_batch(pcm.reshape(-1), np.arange(n + 1, dtype=np.int64) * N, L, S, w)
             return {"feat": torch.as_tensor(r["feat"]), "start_end": torch.as_tensor(r["start_end"]),
                     "n_frames": torch.as_tensor(r["n_frames"])}
@@ -48,13 +52,20 @@ def _worker(rank, ws, port, out_dir):
         X = got["feat"].to(torch.float64).numpy()
 
         def knn(ref, lab, q, k, self_off):
+            if len(q) == 0:
+                return (torch.zeros((0, k), dtype=torch.int32), torch.zeros((0, k), dtype=torch.float64),
+                        torch.zeros(0, dtype=torch.int32))
             i, d, p = oracle.knn(ref, lab.numpy(), q, k, n_classes=3, self_offset=self_off)
             return torch.as_tensor(i), torch.as_tensor(d), torch.as_tensor(p)
 
         idx, dist_, pred = D.knn_sharded(knn, X, labels, X, 3, self_query=True)
+        # one clip over two ranks: rank 1's block is empty and must still join the collectives
+        one = D.extract_sharded(extract, make_shard, 1)
+        i1, d1, p1 = D.knn_sharded(knn, X, labels, X[:1], 3, self_query=False)
         np.savez(os.path.join(out_dir, "rank%d.npz" % rank), feat=got["feat"].numpy(),
                  start_end=got["start_end"].numpy(), n_frames=got["n_frames"].numpy(),
-                 idx=idx.numpy(), dist=dist_.numpy(), pred=pred.numpy())
+                 idx=idx.numpy(), dist=dist_.numpy(), pred=pred.numpy(), one_feat=one["feat"].numpy(),
+                 one_n=one["n_frames"].numpy(), i1=i1.numpy(), d1=d1.numpy(), p1=p1.numpy())
     finally:
         dist.destroy_process_group()
 
@@ -79,3 +90,6 @@ def test_gloo_world2_shard_gather(tmp_path):
         assert np.array_equal(got["n_frames"], full["n_frames"])
         assert np.array_equal(got["idx"], i0) and np.array_equal(got["dist"], d0)
         assert np.array_equal(got["pred"], p0)
+        assert np.array_equal(got["one_feat"], full["feat"][:1]) and np.array_equal(got["one_n"], full["n_frames"][:1])
+        i1, d1, p1 = oracle.knn(full["feat"].astype(np.float64), y, full["feat"][:1].astype(np.float64), 3, n_classes=3)
+        assert np.array_equal(got["i1"], i1) and np.array_equal(got["d1"], d1) and np.array_equal(got["p1"], p1)

@@ -170,3 +170,34 @@ def test_load_dataset_batched(tmp_path):
     import run
     assert run.main(["--data-dir", str(tmp_path), "--results-dir", str(tmp_path / "r2")]) == 0
     assert os.path.exists(tmp_path / "r2" / "exp2_window_comparison" / "results.json")
+
+
+def test_run_py_sample_count_frames(tmp_path):
+    """BASELINE configs[0]: run.py --experiment classifier at 1024 / 512 samples (not an integer-ms
+    setting of config.py:35-40); every feature row against the C oracle at those frame sizes."""
+    import config
+    import run
+    from experiments.run_experiments import list_dataset
+    from src.audio_processing import load_wav_pcm
+    from src.pipeline import create_window
+    from src.synth import make_clip
+    for c in range(3):
+        d = tmp_path / ("c%d" % c)
+        d.mkdir()
+        for j in range(4):
+            _write_wav(d / ("x%d.wav" % j), make_clip(4100 + 10 * c + j, 40000 + 997 * j, label=c, n_classes=3))
+    saved = (config.FRAME_LENGTH, config.FRAME_SHIFT)
+    try:
+        assert run.main(["--data-dir", str(tmp_path), "--results-dir", str(tmp_path / "r"), "--experiment",
+                         "classifier", "--frame-length", "1024", "--frame-shift", "512"]) == 0
+        assert (config.FRAME_LENGTH, config.FRAME_SHIFT) == (1024, 512)
+    finally:
+        config.FRAME_LENGTH, config.FRAME_SHIFT = saved
+    exp = run.last_experiment
+    files, _ = list_dataset(str(tmp_path))
+    assert exp.X.shape == (len(files), 15)
+    w = create_window("hamming", 1024)
+    for row, (f, ci) in enumerate(files):
+        r = oracle.process_clip(load_wav_pcm(f)[0], 1024, 512, w)
+        assert exp.y[row] == ci and rel_ok(exp.X[row], r["feat"]), f
+    assert os.path.exists(tmp_path / "r" / "exp1_classifier_comparison" / "results.json")

@@ -85,3 +85,78 @@ def test_zscore_bit_exact(knn_golden):
         assert np.array_equal(m.cpu().numpy(), mu)
         assert np.array_equal(s.cpu().numpy(), sd)
         assert np.array_equal(zscore_apply(X, m, s).cpu().numpy(), Xn)
+
+
+def _clustered(rng, n, D, classes=10):
+    centres = rng.standard_normal((classes, D)) * 1.5
+    y = rng.integers(0, classes, n).astype(np.int32)
+    X = centres[y] + rng.standard_normal((n, D))
+    return (X - X.mean(0)) / X.std(0), y
+
+
+@pytest.mark.parametrize("Nr,Nq,D,k", [(8000, 1500, 16, 5), (6000, 1000, 32, 3), (5000, 800, 16, 14),
+                                      (4000, 600, 32, 21), (3000, 500, 16, 1)])
+def test_knn_valu_direct_screen(Nr, Nq, D, k):
+    """D = 16 and D = 32 leave no spare column for the expanded form, so they run the direct-form
+    VALU screen (knn_screen<DP, KC, QP>, knn.hip); k = 14 / 21 instantiate KC = 24.  Indices, fp64
+    distances and votes bit-exact against the oracle (sklearn semantics, src/models.py:33-35),
+    plus the self-query exclusion (kneighbors(X=None))."""
+    from src.pipeline import knn_classify
+    rng = np.random.default_rng(Nr + D + k)
+    X, y = _clustered(rng, Nr, D)
+    Q, _ = _clustered(rng, Nq, D)
+    i0, d0, p0 = oracle.knn(X, y, Q, k, n_classes=10, nthreads=8)
+    i1, d1, p1 = knn_classify(X, y, Q, k)
+    assert np.array_equal(i1.cpu().numpy(), i0)
+    assert np.array_equal(d1.cpu().numpy(), d0)
+    assert np.array_equal(p1.cpu().numpy(), p0)
+    lo = Nr // 3
+    i0, d0, p0 = oracle.knn(X, y, X[lo:lo + Nq], k, n_classes=10, self_offset=lo, nthreads=8)
+    i1, d1, p1 = knn_classify(X, y, X[lo:lo + Nq], k, self_offset=lo)
+    assert np.array_equal(i1.cpu().numpy(), i0) and np.array_equal(d1.cpu().numpy(), d0)
+    assert np.array_equal(p1.cpu().numpy(), p0)
+
+
+@pytest.mark.parametrize("k", [14, 21])
+def test_knn_mfma_screen_kc24(k):
+    """The 15-d MFMA screen with k = 14 / 21 (KC = 24: one query tile per wave)."""
+    from src.pipeline import knn_classify
+    rng = np.random.default_rng(k)
+    X, y = _clustered(rng, 12000, 15)
+    i0, d0, p0 = oracle.knn(X, y, X[:1500], k, n_classes=10, self_offset=0, nthreads=8)
+    i1, d1, p1 = knn_classify(X, y, X[:1500], k, self_offset=0)
+    assert np.array_equal(i1.cpu().numpy(), i0)
+    assert np.array_equal(d1.cpu().numpy(), d0)
+    assert np.array_equal(p1.cpu().numpy(), p0)
+
+
+def test_knn_configs4_rank_shard_at_size():
+    """BASELINE configs[4] at full size: the work of one rank of the 8-GPU run -- its 12 500-query
+    shard_range block of the 100 000 x 100 000 15-d self-query (k = 5, self excluded, bench.py's
+    data) -- and the whole 100 000-query self-query on one GPU; 2 000 queries of each checked
+    against the oracle (indices, fp64 distances, votes bit-exact)."""
+    import torch
+    from src.distributed import shard_range
+    from src.pipeline import knn_classify
+    n, k, P, r = 100000, 5, 8, 3
+    rng = np.random.default_rng(0)  # bench.py knn_leg's generator
+    centres = rng.standard_normal((10, 15)) * 1.5
+    y = rng.integers(0, 10, n).astype(np.int32)
+    X = centres[y] + rng.standard_normal((n, 15))
+    X = (X - X.mean(0)) / X.std(0)
+    Xd, yd = torch.as_tensor(X, device="cuda"), torch.as_tensor(y, device="cuda")
+    lo, hi = shard_range(n, r, P)
+    i1, d1, p1 = knn_classify(Xd, yd, Xd[lo:hi], k, self_offset=lo)
+    assert i1.shape == (hi - lo, k)
+    for a in (0, 6000, hi - lo - 1000):  # three 1 000-query blocks of the shard (2 000+ queries)
+        b = a + 1000 if a != 6000 else a + 500
+        i0, d0, p0 = oracle.knn(X, y, X[lo + a:lo + b], k, n_classes=10, self_offset=lo + a, nthreads=16)
+        assert np.array_equal(i1[a:b].cpu().numpy(), i0), a
+        assert np.array_equal(d1[a:b].cpu().numpy(), d0), a
+        assert np.array_equal(p1[a:b].cpu().numpy(), p0), a
+    iA, dA, pA = knn_classify(Xd, yd, Xd, k, self_offset=0)  # the N = 1 configuration
+    assert torch.equal(iA[lo:hi], i1) and torch.equal(dA[lo:hi], d1) and torch.equal(pA[lo:hi], p1)
+    for a in (0, 57000):
+        i0, d0, p0 = oracle.knn(X, y, X[a:a + 500], k, n_classes=10, self_offset=a, nthreads=16)
+        assert np.array_equal(iA[a:a + 500].cpu().numpy(), i0) and np.array_equal(dA[a:a + 500].cpu().numpy(), d0)
+        assert np.array_equal(pA[a:a + 500].cpu().numpy(), p0)
