@@ -40,6 +40,9 @@
 #include "extract_layout.h"
 #include "dsp_device.h"
 
+#ifndef DSP_ABL  // diagnostic ablation builds only (tools/ablate_build.sh; outputs are wrong): skip
+#define DSP_ABL 0 // 1 = R4 frames, 2 = R5 jobs, 4 = R2 sign bits, 8 = VAD pass-A partial moments
+#endif
 #ifndef EXTRACT_R4_KV
 #define EXTRACT_R4_KV 9
 #endif
@@ -451,22 +454,33 @@ __device__ __forceinline__ int vad_partial_word(const ClipRef &cur, int L, int S
     }
     return -1;
 }
-// exact moments (sum k, sum k^2) of elements [e0, e1) of one 32-sample word
+// exact moments (sum k, sum k^2) of elements [e0, e1) of one 32-sample word, branch-free: the
+// range as a bit mask M; pair p's two bits become a 16-bit-lane mask (v_bfe_i32 of each bit,
+// merged by v_bfi), and the pair's masked samples go through one v_dot2 each for sum k and sum k^2
+// (a rolled loop with a branch per element cost ~1.9k instructions per clip, a third of them scalar)
 __device__ __forceinline__ void partial_moments(const short8 (&q)[4], int e0, int e1, int &t1, unsigned long long &t2)
 {
+    const uint32_t hi = e1 >= 32 ? ~0u : (1u << e1) - 1u;
+    const uint32_t M = hi & ~((1u << e0) - 1u);  // e0 < 32
+    const short2v ones = {1, 1};
+    int s1 = 0;
+    unsigned long long s2 = 0;
 #pragma unroll 1
     for (int k = 0; k < 4; k++) {
         const short8 v = k == 0 ? q[0] : k == 1 ? q[1] : k == 2 ? q[2] : q[3];
+        const uint32_t Mk = M >> (8 * k);
 #pragma unroll
-        for (int e = 0; e < 8; e++) {
-            const int x = v[e];
-            const int ee = 8 * k + e;
-            if (ee >= e0 && ee < e1) {
-                t1 += x;
-                t2 += (unsigned)(x * x);
-            }
+        for (int h = 0; h < 4; h++) {  // pair 4k + h: elements 8k + 2h, 8k + 2h + 1
+            const uint32_t b0 = (uint32_t)__builtin_amdgcn_sbfe((int)Mk, 2 * h, 1);
+            const uint32_t b1 = (uint32_t)__builtin_amdgcn_sbfe((int)Mk, 2 * h + 1, 1);
+            const uint32_t m = (b0 & 0x0000FFFFu) | (b1 & 0xFFFF0000u);
+            const short2v dm = __builtin_bit_cast(short2v, __builtin_bit_cast(uint32_t, half_pair(v, h)) & m);
+            s1 = __builtin_amdgcn_sdot2(dm, ones, s1, false);
+            s2 += (unsigned)sq2(dm);
         }
     }
+    t1 += s1;
+    t2 += s2;
 }
 
 // One clip, start to finish; its first RREG words are already in flight into regs (word
@@ -486,6 +500,13 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     float *featb = p.feat + (size_t)i * 15;
     const int16_t *clip_g = p.pcm + cur.base + lead;  // the clip in global memory, sample coords
     STAMP(i, 0);
+#ifdef DSP_STAMPS
+    if (p.stamps) {  // diagnostic build: the clip's loads landed (stamp 13; per wave: 24 + wave)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        STAMP(i, 13);
+        if (lane == 0) p.stamps[(size_t)i * 32 + 24 + wid] = __builtin_amdgcn_s_memtime();
+    }
+#endif
 #ifdef DSP_STAMPS
     if (p.stamps) {  // diagnostic build: the clip's loads landed (stamp 13; per wave: 24 + wave)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -611,7 +632,12 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
 #pragma unroll
         for (int r = 0; r < RREG; r++) {
             const int w = r * NT + tid;
-            if (w < nword) r2_word(&regs[4 * r], w);
+            if (w < nword) {
+                if (DSP_ABL & 4)
+                    c.posw[w] = 0;
+                else
+                    r2_word(&regs[4 * r], w);
+            }
         }
     } else {
 #pragma unroll 1
@@ -653,7 +679,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                     if (tid < 2 * nv) {
                         int t1 = 0;
                         unsigned long long t2 = 0;
-                        if (pa_w >= 0) partial_moments(qa, pa_e0, pa_e1, t1, t2);
+                        if (pa_w >= 0 && !(DSP_ABL & 8)) partial_moments(qa, pa_e0, pa_e1, t1, t2);
                         c.pS1[tid] = t1;
                         c.pS2[tid] = t2;
                     }
@@ -845,7 +871,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     constexpr int R4_KV = EXTRACT_R4_KV;  // vectors per lane in one batch
     const int rl = lane & 15, row = lane >> 4;
     {
-        for (int gi = wid; 4 * gi < F; gi += NWAVE) {
+        for (int gi = wid; !(DSP_ABL & 1) && 4 * gi < F; gi += NWAVE) {
             const int g = 4 * gi + row;
             const bool act = g < F;
             const int gc = act ? g : F - 1;
@@ -919,7 +945,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
             // order statistics by ballot ranks over readlane'd candidates, then mean / std (fp64 sums)
             // and max / min -- no barrier
             // six jobs (median / moments of E, M, ZCR) over the waves
-            for (int job = wid; job < 6; job += NWAVE) {
+            for (int job = wid; !(DSP_ABL & 2) && job < 6; job += NWAVE) {
                 const int q = job % 3;
                 auto get = [&](int j) -> float { return q == 0 ? c.fE[j] : q == 1 ? c.fM[j] : (float)c.fZ[j]; };
                 const bool in0 = lane < F, in1 = lane + 64 < F;

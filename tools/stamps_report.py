@@ -18,9 +18,17 @@ tot = (st[:, 6] - st[:, 0]) / cyc
 print("clip us  p50 %.2f p90 %.2f | first round p50 %.2f (wg<%d %.2f, wg>=%d %.2f) later %.2f" % (
     np.median(tot), np.percentile(tot, 90), np.median(tot[:G]), G // 2, np.median(tot[:G // 2]), G // 2,
     np.median(tot[G // 2:G]), np.median(tot[G:]) if C > G else 0))
-names = {1: "R1 load+stats", 2: "R2 pos", 7: "VAD pass A", 8: "VAD pass B", 3: "p90", 10: "noise+thr", 11: "scan",
+names = {13: "R1 load wait", 1: "R1 stats", 2: "R2 pos", 7: "VAD pass A", 8: "VAD pass B", 3: "p90", 10: "noise+thr", 11: "scan",
          4: "vad out", 12: "R4 frames", 5: "R4 barrier+issue", 9: "R5 jobs", 6: "R5 out"}
-seq = [0, 1, 2, 7, 8, 3, 10, 11, 4, 12, 5, 9, 6]
+seq = [0, 13, 1, 2, 7, 8, 3, 10, 11, 4, 12, 5, 9, 6]
 for a, b in zip(seq, seq[1:]):
     d = (st[:, b] - st[:, a]) / cyc
     print("  %-14s p50 %.2f  oldWG %.2f newWG %.2f" % (names[b], np.median(d), np.median(d[:G // 2]), np.median(d[G // 2:G])))
+
+# per-wave load landing (slots 24..31, diagnostic build): time after the clip start, and the
+# spread between the first and the last wave of the workgroup
+if (st[:, 24:32] > 0).all(axis=1).any():
+    ok = (st[:, 24:32] > 0).all(axis=1) & (st[:, 0] > 0)
+    lw = (st[ok, 24:32] - st[ok, 0:1]) / cyc
+    print("per-wave load landed after clip start us: median of max %.2f, median of min %.2f, per wave p50 %s" % (
+        np.median(lw.max(1)), np.median(lw.min(1)), " ".join("%.2f" % v for v in np.median(lw, 0))))
