@@ -34,7 +34,6 @@
 #include <stdint.h>
 
 #include <algorithm>
-#include <atomic>
 
 #include "dsp_audiorec.h"
 #include "extract_layout.h"
@@ -104,9 +103,9 @@ struct ExtractParams {
     float *seq;
     int ld_seq;
     unsigned long long *stamps;  // diagnostic build only (else null)
-    int queue_slot;              // counter pair g_queue_pool[2 * slot ..]: [0] clips claimed past
-                                 // the first G, [1] workgroups done; both zero at launch, the last
-                                 // workgroup out zeroes them again
+    unsigned *queue;             // caller's clip-queue counter pair (NULL: static split): [0] clips
+                                 // claimed past the first G, [1] workgroups done; both zero at
+                                 // launch, the last workgroup out zeroes them again
     ExtractCarve cv;             // LDS layout, computed on the host (kernel arguments can be
                                  // re-read instead of being held in registers)
 };
@@ -125,12 +124,6 @@ struct Shared {
     int n3, n1, n6, exact, j0, j1, ndefer, next;
 };
 static_assert(sizeof(Shared) <= EXTRACT_SHARED_BYTES, "grow EXTRACT_SHARED_BYTES");
-
-// clip-queue counter pairs, zero-initialised with the code object on each device (no allocation,
-// memset or synchronisation in the entry point); launches take slots round robin on the host, so
-// launches in flight on different streams use different pairs
-static constexpr int QUEUE_SLOTS = 1024;
-__device__ unsigned g_queue_pool[2 * QUEUE_SLOTS];
 
 struct ClipRef {
     int64_t base;  // 8-aligned first sample index of the clip's vectors
@@ -673,76 +666,106 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
         // partial words at its ends, sign changes from the bits.
         // Pass A, one thread per frame end: the partial word's moments (FAST: loaded before the
         // next clip's prefetch; otherwise re-read from L2 here).
-        {
-            if constexpr (!EXACT) {
-                if constexpr (FAST) {
-                    if (tid < 2 * nv) {
-                        int t1 = 0;
-                        unsigned long long t2 = 0;
-                        if (pa_w >= 0 && !(DSP_ABL & 8)) partial_moments(qa, pa_e0, pa_e1, t1, t2);
-                        c.pS1[tid] = t1;
-                        c.pS2[tid] = t2;
-                    }
-                } else {
-                    for (int t = tid; t < 2 * nv; t += NT) {
-                        int e0, e1, t1 = 0;
-                        unsigned long long t2 = 0;
-                        const int pw = vad_partial_word(cur, L, S, nv, t, e0, e1);
-                        if (pw >= 0) {
-                            short8 q[4];
-#pragma unroll
-                            for (int k = 0; k < 4; k++) q[k] = load_vec(p, cur, 4 * pw + k);
-                            partial_moments(q, e0, e1, t1, t2);
-                        }
-                        c.pS1[t] = t1;
-                        c.pS2[t] = t2;
-                    }
+        if constexpr (FAST && !EXACT) {
+            // one lane pair per frame: lane h of pair f owns frame end t = 2f + h = tid (its
+            // partial word was loaded before the barrier), adds that word's exact moments, and
+            // half of the interior word sums and of the sign changes; no pass-A barrier
+            const int f = tid >> 1, lh = tid & 1;
+            const bool act = f < nv;
+            int s1 = 0;
+            unsigned long long s2 = 0;
+            int zc = 0;
+            if (act) {
+                if (pa_w >= 0 && !(DSP_ABL & 8)) partial_moments(qa, pa_e0, pa_e1, s1, s2);
+                const int u0 = lead + f * S, u1 = u0 + L;
+                const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
+                const int wi0 = (u0 & 31) ? wa + 1 : wa, wi1 = (u1 & 31) ? wb - 1 : wb;
+                const int per = (wi1 - wi0 + 2) >> 1;
+                const int ws = wi0 + lh * per, we = min(ws + per - 1, wi1);
+#pragma unroll 4
+                for (int w = ws; w <= we; w++) {
+                    s1 += c.wS1[w];
+                    s2 += c.wS2[w];
                 }
-                __syncthreads();
-                STAMP(i, 7);
+                const int np_ = L - 1, ph = (np_ + 1) >> 1;  // pairs [u0, u1 - 1) in halves
+                const int x0 = u0 + min(lh * ph, np_), x1 = u0 + min((lh + 1) * ph, np_);
+                zc = chg_run(c.posw, x0, x1);
             }
-            // Pass B, one quad per frame: interior word sums and sign changes, each lane a
-            // contiguous quarter
-            const int q4 = tid >> 2, lq = tid & 3;
-            for (int f0 = 0; f0 < nv; f0 += NT / 4) {
-                const int f = f0 + q4;
-                const bool act = f < nv;
-                int s1 = 0;  // |frame sum| <= L * 32768 < 2^31 for L < 65536
-                unsigned long long s2 = 0;
-                int zc = 0;
-                if (act) {
-                    const int u0 = lead + f * S, u1 = u0 + L;
-                    if (!EXACT) {
-                        const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
-                        const int wi0 = (u0 & 31) ? wa + 1 : wa, wi1 = (u1 & 31) ? wb - 1 : wb;
-                        const int per = (wi1 - wi0 + 4) >> 2;
-                        const int ws = wi0 + lq * per, we = min(ws + per - 1, wi1);
-#pragma unroll 3
-                        for (int w = ws; w <= we; w++) {
-                            s1 += c.wS1[w];
-                            s2 += c.wS2[w];
-                        }
-                        if (lq == 0) {
-                            s1 += c.pS1[2 * f] + c.pS1[2 * f + 1];
-                            s2 += c.pS2[2 * f] + c.pS2[2 * f + 1];
+            s1 += dpp_i(s1, DPP_QXOR1);
+            {
+                const unsigned lo = dpp_i((int)(unsigned)s2, DPP_QXOR1), hi = dpp_i((int)(unsigned)(s2 >> 32), DPP_QXOR1);
+                s2 += ((unsigned long long)hi << 32) | lo;
+            }
+            zc += dpp_i(zc, DPP_QXOR1);
+            if (act && lh == 0) {
+                c.vE[f] = energy_from_moments(s2, s1, L, t0, mq - (double)t0, invM2);
+                c.vZ[f] = zc;
+            }
+            STAMP(i, 7);
+        } else {
+            {
+                if constexpr (!EXACT) {
+                    {  // generic layout: the partial words re-read from L2 here
+                        for (int t = tid; t < 2 * nv; t += NT) {
+                            int e0, e1, t1 = 0;
+                            unsigned long long t2 = 0;
+                            const int pw = vad_partial_word(cur, L, S, nv, t, e0, e1);
+                            if (pw >= 0) {
+                                short8 q[4];
+    #pragma unroll
+                                for (int k = 0; k < 4; k++) q[k] = load_vec(p, cur, 4 * pw + k);
+                                partial_moments(q, e0, e1, t1, t2);
+                            }
+                            c.pS1[t] = t1;
+                            c.pS2[t] = t2;
                         }
                     }
-                    const int np_ = L - 1, pq = (np_ + 3) >> 2;  // pairs [u0, u1 - 1) in quarters
-                    const int x0 = u0 + min(lq * pq, np_), x1 = u0 + min((lq + 1) * pq, np_);
-                    zc = chg_run(c.posw, x0, x1);
+                    __syncthreads();
+                    STAMP(i, 7);
                 }
-                s1 = dpp_quad_reduce(s1, OpAdd());
-                s2 = dpp_quad_sum64(s2);
-                zc = dpp_quad_reduce(zc, OpAdd());
-                if (act && lq == 0) {
-                    if (!FAST) c.rank[f] = 0;
-                    c.vE[f] = EXACT ? np_energy_exact(clip_g, f * S, L, mq, Mp)
-                                    : energy_from_moments(s2, s1, L, t0, mq - (double)t0, invM2);
-                    c.vZ[f] = zc;
+                // Pass B, one quad per frame: interior word sums and sign changes, each lane a
+                // contiguous quarter
+                const int q4 = tid >> 2, lq = tid & 3;
+                for (int f0 = 0; f0 < nv; f0 += NT / 4) {
+                    const int f = f0 + q4;
+                    const bool act = f < nv;
+                    int s1 = 0;  // |frame sum| <= L * 32768 < 2^31 for L < 65536
+                    unsigned long long s2 = 0;
+                    int zc = 0;
+                    if (act) {
+                        const int u0 = lead + f * S, u1 = u0 + L;
+                        if (!EXACT) {
+                            const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
+                            const int wi0 = (u0 & 31) ? wa + 1 : wa, wi1 = (u1 & 31) ? wb - 1 : wb;
+                            const int per = (wi1 - wi0 + 4) >> 2;
+                            const int ws = wi0 + lq * per, we = min(ws + per - 1, wi1);
+    #pragma unroll 3
+                            for (int w = ws; w <= we; w++) {
+                                s1 += c.wS1[w];
+                                s2 += c.wS2[w];
+                            }
+                            if (lq == 0) {
+                                s1 += c.pS1[2 * f] + c.pS1[2 * f + 1];
+                                s2 += c.pS2[2 * f] + c.pS2[2 * f + 1];
+                            }
+                        }
+                        const int np_ = L - 1, pq = (np_ + 3) >> 2;  // pairs [u0, u1 - 1) in quarters
+                        const int x0 = u0 + min(lq * pq, np_), x1 = u0 + min((lq + 1) * pq, np_);
+                        zc = chg_run(c.posw, x0, x1);
+                    }
+                    s1 = dpp_quad_reduce(s1, OpAdd());
+                    s2 = dpp_quad_sum64(s2);
+                    zc = dpp_quad_reduce(zc, OpAdd());
+                    if (act && lq == 0) {
+                        if (!FAST) c.rank[f] = 0;
+                        c.vE[f] = EXACT ? np_energy_exact(clip_g, f * S, L, mq, Mp)
+                                        : energy_from_moments(s2, s1, L, t0, mq - (double)t0, invM2);
+                        c.vZ[f] = zc;
+                    }
                 }
             }
-            __syncthreads();
         }
+        __syncthreads();
         STAMP(i, 8);
         {
             // p90 order statistics (:198)
@@ -1168,14 +1191,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     __syncthreads();
     WG_CK(20);
 
-    // Clip blockIdx.x first, then clips claimed from a launch-wide counter, so that workgroups
-    // whose clips run short take more of them (a static i, i + G, ... split ends on the slowest
-    // workgroup: 3.19-3.98 ms spread at 100 000 clips).  Thread 0 claims the next clip right after
-    // issuing the current clip's loads; the claim's latency hides behind the clip.  A workgroup
-    // claims only while its near-tie list has room for the current and the claimed clip, and the
-    // host keeps a launch at <= G * EXTRACT_DEFER_CAP / 2 clips, so the list never overflows and
-    // some workgroup can always claim what is left.
-    unsigned *const queue = g_queue_pool + 2 * p.queue_slot;
+    // Clip blockIdx.x first, then clips claimed from the caller's launch-wide counter (p.queue), so
+    // that workgroups whose clips run short take more of them (a static i, i + G, ... split ends on
+    // the slowest workgroup: 3.19-3.98 ms spread at 100 000 clips); without a counter, the static
+    // split.  Thread 0 claims the next clip right after issuing the current clip's loads; the
+    // claim's latency hides behind the clip.  A workgroup claims only while its near-tie list has
+    // room for the current and the claimed clip, and the host keeps a launch at <= G *
+    // EXTRACT_DEFER_CAP / 2 clips, so the list never overflows and some workgroup can always claim
+    // what is left (statically, a workgroup gets <= EXTRACT_DEFER_CAP / 2 clips).
+    unsigned *const queue = p.queue;
+    auto next_clip = [&](int i) -> unsigned {  // thread 0 only
+        return queue ? (unsigned)G + __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     : (unsigned)(i + G);
+    };
     short8 regs[NRV];
     bool inflight = false;  // regs already hold clip i's loads (issued by the previous clip's R4)
     for (int i = blockIdx.x; i < p.B;) {
@@ -1183,13 +1211,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
         unsigned claim = 0x7fffffffu;
         if (!cur.ok) {
             __syncthreads();  // everyone has read sh->next (the ok path has barriers in clip_body)
-            if (tid == 0) claim = (unsigned)G + __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0) claim = next_clip(i);
             write_bad_clip(p, i, tid);
             inflight = false;
         } else {
             if (!inflight) issue_clip(regs, p, cur);
-            if (tid == 0 && sh->ndefer < EXTRACT_DEFER_CAP - 1)
-                claim = (unsigned)G + __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0 && (!queue || sh->ndefer < EXTRACT_DEFER_CAP - 1)) claim = next_clip(i);
             c.stamp_clip = i;
             const bool done = clip_body<false, FAST>(p, c, i, cur, regs, claim);
             if (!done && tid == 0) c.defer[sh->ndefer++] = i;
@@ -1209,7 +1236,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     }
     // the last workgroup out resets the queue for the next launch on the stream: every claim of
     // every workgroup precedes its increment of the done count
-    if (tid == 0) {
+    if (tid == 0 && queue) {
         const unsigned d = __hip_atomic_fetch_add(queue + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         if (d == (unsigned)G - 1) {
             __hip_atomic_store(queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1238,23 +1265,21 @@ extern "C" size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int f
     return c.total <= EXTRACT_LDS_LIMIT ? (size_t)c.total : 0;
 }
 
-// CU count per device (the persistent grid), cached on first use of each device; the next
-// clip-queue slot (dsp::g_queue_pool)
+// CU count per device (the persistent grid), cached on first use of each device
 static int g_num_cus[64];
 static_assert(EXTRACT_DEFER_CAP >= 2, "the claim rule keeps room for two clips");
-static std::atomic<unsigned> g_queue_next{0};
 
 extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, int B,
                                     int64_t max_len, int frame_length, int frame_shift,
                                     const double *window, int do_vad, double hi, double lo,
                                     double zr, float *feat, int32_t *start_end, int32_t *n_frames,
                                     int32_t *status, double *vad_energy, int32_t *vad_zcr,
-                                    int ld_vad, float *seq, int ld_seq, void *stream)
+                                    int ld_vad, float *seq, int ld_seq, void *queue_ws, void *stream)
 {
     if (B < 0 || !offsets || !window || !feat || !start_end || !n_frames || !status)
         return DSP_ERR_ARGS;
     if (frame_length < 1 || frame_shift < 1 || max_len < 1) return DSP_ERR_ARGS;
-    if (((uintptr_t)pcm & 15) != 0) return DSP_ERR_ARGS;
+    if (((uintptr_t)pcm & 15) != 0 || ((uintptr_t)queue_ws & 3) != 0) return DSP_ERR_ARGS;
     if ((vad_energy == nullptr) != (vad_zcr == nullptr)) return DSP_ERR_ARGS;
     if (vad_energy && ld_vad < 1) return DSP_ERR_ARGS;
     if (seq && ld_seq < 1) return DSP_ERR_ARGS;
@@ -1295,6 +1320,7 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     p.seq = seq;
     p.ld_seq = ld_seq;
     p.stamps = (unsigned long long *)g_stamp_buffer;
+    p.queue = (unsigned *)queue_ws;
     p.cv = extract_carve((int)max_len, frame_length, frame_shift, EXTRACT_DEFER_CAP);
     // persistent grid: two workgroups per CU when their LDS fits (one otherwise), each walking
     // clip blockIdx first, then clips from the launch's queue; the compile-time layout whenever
@@ -1323,7 +1349,6 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
         if (seq) q.seq = seq + b0 * ld_seq * 3;
         if (q.stamps) q.stamps = p.stamps + 32 * b0;
         const int grid = nb < slots ? nb : slots;
-        q.queue_slot = (int)(g_queue_next.fetch_add(1, std::memory_order_relaxed) % dsp::QUEUE_SLOTS);
         if (fast)
             hipLaunchKernelGGL(dsp::extract_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch, (hipStream_t)stream, q);
         else

@@ -24,6 +24,7 @@ CLIP_NO_FRAMES = 3
 CLIP_TOO_LONG = 4
 CLIP_UNCERTIFIED = 5  # reserved (never produced)
 CLIP_FLAG_VAD_EXACT = 0x100
+ABI_VERSION = 2  # include/dsp_audiorec.h DSP_ABI_VERSION this binding is typed for
 
 EXPORTS = ("dsp_extract_lds_bytes", "dsp_extract_features", "dsp_extract_general_workspace_bytes",
            "dsp_extract_general", "dsp_knn_workspace_bytes",
@@ -57,7 +58,7 @@ def load_library(path=LIB_PATH):
     L.dsp_extract_lds_bytes.argtypes = [i64, i32, i32]
     L.dsp_extract_features.restype = i32
     L.dsp_extract_features.argtypes = [vp, vp, i32, i64, i32, i32, vp, i32, dbl, dbl, dbl,
-                                       vp, vp, vp, vp, vp, vp, i32, vp, i32, vp]
+                                       vp, vp, vp, vp, vp, vp, i32, vp, i32, vp, vp]
     L.dsp_extract_general_workspace_bytes.restype = sz
     L.dsp_extract_general_workspace_bytes.argtypes = [i64, i64, i32, i32]
     L.dsp_extract_general.restype = i32
@@ -73,6 +74,8 @@ def load_library(path=LIB_PATH):
     L.dsp_zscore_apply.argtypes = [vp, i64, i32, vp, vp, vp, vp]
     L.dsp_abi_version.restype = i32
     L.dsp_abi_version.argtypes = []
+    if L.dsp_abi_version() != ABI_VERSION:
+        raise HipError("%s has ABI %d, this binding expects %d: rebuild it" % (path, L.dsp_abi_version(), ABI_VERSION))
     _lib = L
     return L
 

@@ -141,9 +141,12 @@ class FeatureExtractor:
                 _hip.ptr(sq), lds_)
         cap = 0 if wide else self.fused_cap()
         if not wide and B > 0 and cap > 0:
+            # the launch's own zeroed clip-queue counter pair: a capture of this call in a graph
+            # gets its own from the graph's pool, so concurrent launches never share one
+            queue = torch.zeros(2, dtype=torch.int32, device=d)
             rc = _hip.lib().dsp_extract_features(
                 _hip.ptr(pcm), _hip.ptr(off), B, min(max_len, cap), self.L, self.S,
-                _hip.ptr(self.window), *args, _hip.stream_handle(d))
+                _hip.ptr(self.window), *args, _hip.ptr(queue), _hip.stream_handle(d))
             _hip.check(rc, "dsp_extract_features")
         if B > 0 and (wide or max_len > cap):
             # the clips the fused kernel cannot hold (longer than cap, or every clip of an int32

@@ -12,6 +12,9 @@
  *  - Every launch is stream-ordered on `stream` (a hipStream_t passed as void*;
  *    NULL = the legacy default stream).  No entry point allocates, frees, copies
  *    to the host or synchronises, so all of them may be captured in a hipGraph.
+ *  - Scratch buffers (workspace, queue_ws) belong to one launch at a time, like any
+ *    scratch: launches that may run concurrently (other streams, other instances of a
+ *    captured graph) need their own.  No entry point keeps state between launches.
  *  - Return value: 0 on success, a DSP_ERR_* code (argument checks, done on the
  *    host before launching), or DSP_ERR_HIP + hipError_t when a launch fails.
  *  - Per-item failures (the reference raises ValueError and its callers skip the
@@ -27,7 +30,7 @@
 extern "C" {
 #endif
 
-#define DSP_ABI_VERSION 1
+#define DSP_ABI_VERSION 2  /* 2: dsp_extract_features takes the clip-queue scratch (queue_ws) */
 
 /* return codes */
 #define DSP_OK 0
@@ -45,7 +48,8 @@ extern "C" {
                                  processes such clips) */
 #define DSP_CLIP_UNCERTIFIED 5 /* reserved: an endpoint decision that could not be certified.
                                   Never produced: a workgroup claims clips only while its
-                                  near-tie list has room and launches hold at most
+                                  near-tie list has room (statically it gets at most half the
+                                  list's capacity) and launches hold at most
                                   G x EXTRACT_DEFER_CAP / 2 clips, so every near tie is redone
                                   on the exact path */
 /* status[b] flag bits (informational) */
@@ -85,12 +89,19 @@ size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int frame_shift)
  * seq       (optional, may be NULL): float32 [B, ld_seq, 3] per-frame (E, M, ZCR) -- the
  *           'sequence' method of extract_features_from_frames (:114-129); frames beyond
  *           ld_seq are dropped.
+ * queue_ws  (optional, may be NULL): 8 bytes of device scratch, zero before the launch, the
+ *           counter pair of the dynamic clip queue (persistent workgroups claim the next clip
+ *           from it, so fast workgroups take more clips); the launch leaves it zero again, so it
+ *           can be reused by the next launch on the same stream.  NULL: a static round-robin
+ *           split of the clips over the workgroups (same results, ~6% slower at 100k clips).
+ *           One launch at a time per queue_ws (see Conventions).
  */
 int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, int B, int64_t max_len,
                          int frame_length, int frame_shift, const double *window, int do_vad,
                          double hi, double lo, double zr, float *feat, int32_t *start_end,
                          int32_t *n_frames, int32_t *status, double *vad_energy,
-                         int32_t *vad_zcr, int ld_vad, float *seq, int ld_seq, void *stream);
+                         int32_t *vad_zcr, int ld_vad, float *seq, int ld_seq, void *queue_ws,
+                         void *stream);
 
 /*
  * dsp_extract_general -- the same pipeline for clips outside the fused kernel's on-chip plan:
@@ -121,8 +132,15 @@ int dsp_extract_general(const void *pcm, int sample_bytes, const int64_t *offset
  * KNN -- KNeighborsClassifier(n_neighbors=k) as configured in src/models.py:33-35 and used by
  * TraditionalClassifier.fit/predict (:52-58): exact Euclidean k nearest neighbours of each query
  * row among the reference rows, ascending distance, then a uniform majority vote in which the
- * smallest label wins ties (scipy.stats.mode).  Screening runs in fp32 on VALU (no MFMA);
- * survivors are re-ranked with the reference's own fp64 distance (sequential sum of squared
+ * smallest label wins ties (scipy.stats.mode).  Screening runs in fp32: for D < 16 / D < 32
+ * (the 15-d features) in the expanded form |q|^2 + q'.r' on the matrix cores
+ * (v_mfma_f32_16x16x4_f32, f32 in / f32 accumulate -- a deliberate departure from north_star's
+ * "no MFMA", measured 6.9 -> 5.7 ms at 100k x 100k), for D = 16 / 32 in the
+ * direct form (q - r)^2 on the VALU, for D > 32 in the direct form in chunks of 16.  The screen
+ * only nominates candidates: its error bound (knn.hip knn_err_coeffs) holds for any summation
+ * order inside an MFMA with at most one rounding per product and per addition, so the
+ * certification below does not rest on the matrix core matching an fmaf chain bit for bit.
+ * Survivors are re-ranked with the reference's own fp64 distance (sequential sum of squared
  * differences, no FMA, sqrt), and any query whose fp32 screen cannot certify the fp64 top-k is
  * re-solved exhaustively in fp64 on the device.  Exact-distance ties are ordered by smaller
  * reference index.

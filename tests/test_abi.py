@@ -58,12 +58,13 @@ def test_host_argument_checks(lib):
     buf = ctypes.create_string_buffer(64)
     p = ctypes.cast(buf, ctypes.c_void_p)
     p2 = ctypes.c_void_p(p.value + 2)  # misaligned pcm
-    args = lambda pcm, B, L=1102, S=441, feat=p: (pcm, p, B, 44100, L, S, p, 1, 0.5, 0.1, 1.5,
-                                                   feat, p, p, p, None, None, 0, None, 0, None)
+    args = lambda pcm, B, L=1102, S=441, feat=p, q=None: (pcm, p, B, 44100, L, S, p, 1, 0.5, 0.1, 1.5,
+                                                         feat, p, p, p, None, None, 0, None, 0, q, None)
     assert f(*args(p, -1)) == _hip.DSP_ERR_ARGS
     assert f(*args(p, 4, feat=None)) == _hip.DSP_ERR_ARGS
     assert f(*args(p2, 4)) == _hip.DSP_ERR_ARGS
     assert f(*args(p, 4, L=0)) == _hip.DSP_ERR_ARGS
+    assert f(*args(p, 4, q=p2)) == _hip.DSP_ERR_ARGS  # misaligned clip-queue scratch
     assert f(*args(p, 0)) == _hip.DSP_OK  # empty batch: nothing to launch
     assert lib.dsp_knn_workspace_bytes(100, 100, 4097, 5) == 0
     assert lib.dsp_knn_workspace_bytes(100, 100, 33, 5) > 0  # high-dimensional screen

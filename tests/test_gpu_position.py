@@ -111,3 +111,47 @@ def test_sharded_extraction_odd_shard_size():
     sh = fx(shifted, off + 5)
     for k in full:
         assert torch.equal(sh[k], full[k]), k
+
+
+def test_two_streams_concurrent_and_static_split():
+    """Two extractions in flight at once on two streams (each call has its own clip-queue
+    scratch), and the C ABI's static split (queue_ws = NULL): every result equals the oracle /
+    the queued launch bit for bit."""
+    import torch
+    from src import _hip
+    from src.pipeline import FeatureExtractor, create_window
+    from src.synth import make_batch
+    xa = torch.as_tensor(make_batch(3000, base_seed=31)).cuda()
+    xb = torch.as_tensor(make_batch(2500, base_seed=77, n_samples=30000)).cuda()
+    fa = FeatureExtractor(L, S, "hamming", True)
+    fb = FeatureExtractor(1024, 512, "hanning", True)
+    ref_a = {k: v.clone() for k, v in fa(xa).items()}
+    ref_b = {k: v.clone() for k, v in fb(xb).items()}
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for _ in range(5):
+        with torch.cuda.stream(sa):
+            oa = fa(xa)
+        with torch.cuda.stream(sb):
+            ob = fb(xb)
+        torch.cuda.synchronize()
+        for k in ref_a:
+            assert torch.equal(oa[k], ref_a[k]), k
+            assert torch.equal(ob[k], ref_b[k]), k
+    host = xa.cpu().numpy()
+    for i in range(0, 3000, 211):
+        r = oracle.process_clip(host[i], L, S, create_window("hamming", L))
+        assert tuple(ref_a["start_end"][i].tolist()) == (r["start"], r["end"])
+        assert not feat_close(ref_a["feat"][i].cpu().numpy(), r["feat"]).any()
+    # queue_ws = NULL: the static split, same bits
+    out = {k: torch.empty_like(v) for k, v in ref_a.items()}
+    flat = xa.reshape(-1)
+    off = torch.arange(3001, dtype=torch.int64, device="cuda") * xa.shape[1]
+    P = _hip.ptr
+    rc = _hip.lib().dsp_extract_features(P(flat), P(off), 3000, xa.shape[1], L, S, P(fa.window), 1, 0.5, 0.1, 1.5,
+                                         P(out["feat"]), P(out["start_end"]), P(out["n_frames"]), P(out["status"]),
+                                         None, None, 0, None, 0, None, _hip.stream_handle())
+    _hip.check(rc, "dsp_extract_features")
+    torch.cuda.synchronize()
+    for k in ref_a:
+        assert torch.equal(out[k], ref_a[k]), k
