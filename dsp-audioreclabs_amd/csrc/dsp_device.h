@@ -439,7 +439,9 @@ __device__ __forceinline__ unsigned shfl_xor_k(unsigned v, int m, int lane)
     switch (m) {
     case 1: return (unsigned)__builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);
     case 2: return (unsigned)__builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);
-    case 4: return (unsigned)__builtin_amdgcn_ds_swizzle(x, 0x101F);
+    case 4:  // i ^ 4 = (i ^ 7) ^ 3: row_half_mirror, then quad_perm [3,2,1,0] (two DPP moves, no LDS)
+        return (unsigned)__builtin_amdgcn_update_dpp(0, __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false),
+                                                     0x1B, 0xF, 0xF, false);
     case 8: return (unsigned)__builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);
     case 16: {
         const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);

@@ -500,13 +500,6 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
         if (lane == 0) p.stamps[(size_t)i * 32 + 24 + wid] = __builtin_amdgcn_s_memtime();
     }
 #endif
-#ifdef DSP_STAMPS
-    if (p.stamps) {  // diagnostic build: the clip's loads landed (stamp 13; per wave: 24 + wave)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        STAMP(i, 13);
-        if (lane == 0) p.stamps[(size_t)i * 32 + 24 + wid] = __builtin_amdgcn_s_memtime();
-    }
-#endif
 
     // ---- R1: integer sum / min / max; exact moments per 32-sample word -----------------------
     int K = 0;  // <= RREG * 32 * 32768 per thread (longer clips: one word per loop trip)

@@ -455,8 +455,37 @@ __device__ int vote(const int *il, int k, const int32_t *labels)
 
 static constexpr int KMAX = 32;
 
-template <int KC>
-__global__ void knn_merge(const double *__restrict__ ref, const double *__restrict__ query,
+// the KM smallest (distance, index) pairs in ascending order, fixed length (no register array is
+// indexed at run time, so the lists stay in registers)
+template <int KM>
+__device__ __forceinline__ void topk_fixed_insert(double (&dl)[KM], int (&il)[KM], double d, int r)
+{
+    if (!cand_less(d, r, dl[KM - 1], il[KM - 1])) return;
+#pragma unroll
+    for (int i = KM - 1; i > 0; i--) {
+        const bool shift = cand_less(d, r, dl[i - 1], il[i - 1]);
+        const bool here = !shift && cand_less(d, r, dl[i], il[i]);
+        dl[i] = shift ? dl[i - 1] : here ? d : dl[i];
+        il[i] = shift ? il[i - 1] : here ? r : il[i];
+    }
+    if (cand_less(d, r, dl[0], il[0])) {
+        dl[0] = d;
+        il[0] = r;
+    }
+}
+template <int KM, typename T>
+__device__ __forceinline__ T kth_of(const T (&a)[KM], int k)  // a[k - 1], k run-time
+{
+    T v = a[0];
+#pragma unroll
+    for (int i = 1; i < KM; i++) v = (i == k - 1) ? a[i] : v;
+    return v;
+}
+
+// One thread per query, lists of KM >= k entries (k <= 8: 8) held in registers; each split's KC
+// candidates are loaded together.
+template <int KC, int KM>
+__global__ __launch_bounds__(64) void knn_merge(const double *__restrict__ ref, const double *__restrict__ query,
                           int64_t Nr, int64_t Nq, int D, int k, int nsplit, int64_t self_offset,
                           const float *__restrict__ cand_d, const int *__restrict__ cand_i,
                           const unsigned int *maxnorm_bits, double err_rel, double err_abs,
@@ -467,10 +496,10 @@ __global__ void knn_merge(const double *__restrict__ ref, const double *__restri
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= Nq) return;
     const double *qx = query + q * D;
-    double dl[KMAX];
-    int il[KMAX];
+    double dl[KM];
+    int il[KM];
 #pragma unroll
-    for (int i = 0; i < KMAX; i++) {
+    for (int i = 0; i < KM; i++) {
         dl[i] = INFINITY;
         il[i] = 0x7fffffff;
     }
@@ -480,62 +509,92 @@ __global__ void knn_merge(const double *__restrict__ ref, const double *__restri
     // sum (direct or expanded form), coefficients from the host (knn_err_coeffs)
     const double rmax = (double)__uint_as_float(*maxnorm_bits);
     auto err = [&](double d) { return err_rel * d + err_abs * (qn + rmax) + 1e-30; };
+    const int64_t self = self_offset >= 0 ? self_offset + q : -1;
     // pass 1 (fp32 only): the k-th smallest screened distance t32 and the screening cut-off of
     // every split whose candidate list is full
-    float k32[KMAX];
+    float k32[KM];
 #pragma unroll
-    for (int i = 0; i < KMAX; i++) k32[i] = INFINITY;
-    float cut = INFINITY;
+    for (int i = 0; i < KM; i++) k32[i] = INFINITY;
+    float kth = INFINITY, cut = INFINITY;
     for (int s = 0; s < nsplit; s++) {
         const size_t o = ((size_t)s * Nq + q) * KC;
+        int rr[KC];
+        float dd[KC];
 #pragma unroll
         for (int i = 0; i < KC; i++) {
-            const int r = cand_i[o + i];
-            const float d = cand_d[o + i];
-            if (r < 0 || (self_offset >= 0 && r == self_offset + q)) continue;
-            if (d < k32[k - 1]) {  // sorted insert into the k smallest
-                float v = d;
-                for (int j = 0; j < k; j++) {
-                    const float lo = fminf(v, k32[j]);
-                    v = fmaxf(v, k32[j]);
-                    k32[j] = lo;
-                }
-            }
+            rr[i] = cand_i[o + i];
+            dd[i] = cand_d[o + i];
         }
-        if (cand_i[o + KC - 1] >= 0) cut = fminf(cut, cand_d[o + KC - 1]);
+#pragma unroll
+        for (int i = 0; i < KC; i++) {
+            if (rr[i] < 0 || rr[i] == self || !(dd[i] < kth)) continue;
+            float v = dd[i];  // sorted insert into the KM smallest
+#pragma unroll
+            for (int j = 0; j < KM; j++) {
+                const float lo = fminf(v, k32[j]);
+                v = fmaxf(v, k32[j]);
+                k32[j] = lo;
+            }
+            kth = kth_of<KM>(k32, k);
+        }
+        if (rr[KC - 1] >= 0) cut = fminf(cut, dd[KC - 1]);
     }
     // pass 2: fp64 re-rank (sklearn's own distance) of the candidates that can still be among the
     // k nearest: a candidate with d - err(d) > t32 + err(t32) is farther (in fp64) than the k
     // candidates at or below t32
-    const double t32 = (double)k32[k - 1];
+    const double t32 = (double)kth;
     const double keep = t32 < INFINITY ? t32 + err(t32) : INFINITY;
     for (int s = 0; s < nsplit; s++) {
         const size_t o = ((size_t)s * Nq + q) * KC;
+        int rr[KC];
+        float dd[KC];
+#pragma unroll
         for (int i = 0; i < KC; i++) {
-            const int r = cand_i[o + i];
-            const double d = (double)cand_d[o + i];
-            if (r < 0 || (self_offset >= 0 && r == self_offset + q)) continue;
-            if (d - err(d) > keep) continue;
-            topk64_insert<KMAX>(dl, il, k, rdist64(qx, ref + (int64_t)r * D, D), r);
+            rr[i] = cand_i[o + i];
+            dd[i] = cand_d[o + i];
+        }
+#pragma unroll
+        for (int i = 0; i < KC; i++) {
+            const double d = (double)dd[i];
+            if (rr[i] < 0 || rr[i] == self || d - err(d) > keep) continue;
+            topk_fixed_insert<KM>(dl, il, rdist64(qx, ref + (int64_t)rr[i] * D, D), rr[i]);
         }
     }
     // certification: any row that was screened out has fp32 distance >= cut; its true fp64
     // squared distance is >= cut - tol (fp32 rounding of inputs and of the sum).
     const double tol = err((double)cut);
-    const bool ok = !(cut < INFINITY) || ((double)cut - tol > dl[k - 1]);
+    const bool ok = !(cut < INFINITY) || ((double)cut - tol > kth_of<KM>(dl, k));
     if (!ok) {
         const int slot = atomicAdd(fb_count, 1);
         fb_list[slot] = (int)q;
         return;
     }
-    int outi[KMAX];
-    for (int i = 0; i < k; i++) {
+    int outi[KM];
+#pragma unroll
+    for (int i = 0; i < KM; i++) {
         const bool valid = dl[i] < INFINITY;
         outi[i] = valid ? il[i] : -1;
-        idx[q * k + i] = outi[i];
-        dist[q * k + i] = valid ? sqrt(dl[i]) : INFINITY;
+        if (i < k) {
+            idx[q * k + i] = outi[i];
+            dist[q * k + i] = valid ? sqrt(dl[i]) : INFINITY;
+        }
     }
-    if (pred && labels) pred[q] = vote(outi, k, labels);
+    if (pred && labels) {  // scipy.stats.mode of the k labels: the smallest most frequent
+        int best = -1, bestc = 0;
+#pragma unroll
+        for (int a = 0; a < KM; a++) {
+            if (a >= k || outi[a] < 0) continue;
+            const int la = labels[outi[a]];
+            int cnt = 0;
+#pragma unroll
+            for (int b2 = 0; b2 < KM; b2++) cnt += b2 < k && outi[b2] >= 0 && labels[outi[b2]] == la;
+            if (cnt > bestc || (cnt == bestc && la < best)) {
+                bestc = cnt;
+                best = la;
+            }
+        }
+        pred[q] = best;
+    }
 }
 
 // exhaustive fp64 for the queries the screen could not certify: one workgroup per query
@@ -737,13 +796,25 @@ void launch_screen(dim3 g, hipStream_t s, const float *r, int64_t Nr, const floa
 }
 
 template <int KC>
-void launch_merge(dim3 g, dim3 b, hipStream_t s, const double *ref, const double *query,
-                  int64_t Nr, int64_t Nq, int D, int k, int nsplit, int64_t self, const float *cd,
-                  const int *ci, const unsigned *mx, double er, double ea, const int32_t *lbl,
-                  int32_t *idx, double *dist, int32_t *pred, int *fbc, int *fbl)
+void launch_merge(hipStream_t s, const double *ref, const double *query, int64_t Nr, int64_t Nq, int D, int k,
+                  int nsplit, int64_t self, const float *cd, const int *ci, const unsigned *mx, double er,
+                  double ea, const int32_t *lbl, int32_t *idx, double *dist, int32_t *pred, int *fbc, int *fbl)
 {
-    hipLaunchKernelGGL((dsp::knn_merge<KC>), g, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self,
-                       cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl);
+    // 64-thread workgroups: 12 500 queries (one rank of the 8-GPU self-query) are 196 of them
+    const dim3 g((unsigned)((Nq + 63) / 64)), b(64);
+    // KC >= k + KNN_SLACK, so KC = 8 implies k <= 8 and KC = 16 implies k <= 16
+    if (k <= 8) {
+        hipLaunchKernelGGL((dsp::knn_merge<KC, 8>), g, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self, cd, ci, mx,
+                           er, ea, lbl, idx, dist, pred, fbc, fbl);
+    } else if (k <= 16) {
+        if constexpr (KC >= 16)
+            hipLaunchKernelGGL((dsp::knn_merge<KC, 16>), g, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self, cd, ci,
+                               mx, er, ea, lbl, idx, dist, pred, fbc, fbl);
+    } else {
+        if constexpr (KC >= 24)
+            hipLaunchKernelGGL((dsp::knn_merge<KC, 32>), g, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self, cd, ci,
+                               mx, er, ea, lbl, idx, dist, pred, fbc, fbl);
+    }
 }
 
 // err(d) = er * d + ea * (|q|^2 + max |r|^2) bounds |fp32 screened - fp64| distance.
@@ -836,12 +907,11 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
     double er, ea;
     knn_err_coeffs(l, D, er, ea);
     const int32_t *lbl = pred ? ref_labels : nullptr;
-    const dim3 mg((unsigned)((Nq + 127) / 128)), mb(128);
     switch (l.KC) {
-    case 8: launch_merge<8>(mg, mb, s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
-    case 16: launch_merge<16>(mg, mb, s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
-    case 24: launch_merge<24>(mg, mb, s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
-    default: launch_merge<36>(mg, mb, s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
+    case 8: launch_merge<8>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
+    case 16: launch_merge<16>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
+    case 24: launch_merge<24>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
+    default: launch_merge<36>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
     }
     const unsigned fbgrid = (unsigned)(Nq < 512 ? Nq : 512);
     hipLaunchKernelGGL(dsp::knn_fallback, dim3(fbgrid), dim3(dsp::FB_T), 0, s, ref, query, Nr, D,
