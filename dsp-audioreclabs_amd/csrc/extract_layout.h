@@ -3,8 +3,8 @@
 // The clip itself is NOT in LDS: it is held in registers (EXTRACT_RREG 32-sample words per
 // thread) for the two passes that need every sample, and re-read from L2 by the phases that need
 // a few (crop frames, partial words at VAD frame edges).  LDS holds per-word summaries (positive-
-// sample bits, exact moments) and the small per-frame arrays, ~36 KB for a 1 s clip, so two
-// workgroups share a CU.
+// sample bits, exact moments), the window table and the small per-frame arrays (~54 KB in the
+// compile-time layout), so two workgroups share a CU.
 #ifndef DSP_EXTRACT_LAYOUT_H
 #define DSP_EXTRACT_LAYOUT_H
 

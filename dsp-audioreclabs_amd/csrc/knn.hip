@@ -184,11 +184,20 @@ __global__ __launch_bounds__(KNN_TQ) void knn_screen(const float *__restrict__ r
 // of the union -- and inserts only when some lane has a distance below it.  Padding rows carry an
 // infinite |r|^2 (distance +inf); the query's own row (self_offset) is masked only in the steps
 // that can hold one of the wave's 32 own rows.
-static constexpr int MQ_W = 2;                         // waves per workgroup
+#ifndef KNN_MQ_W
+#define KNN_MQ_W 2
+#endif
+#ifndef KNN_MQ_T
+#define KNN_MQ_T 2
+#endif
+#ifndef KNN_MQ_TR
+#define KNN_MQ_TR 256
+#endif
+static constexpr int MQ_W = KNN_MQ_W;                  // waves per workgroup
 // query tiles (16 queries) per wave: two while the lists are short, one for long lists (k > 13)
-__host__ __device__ constexpr int mq_tiles(int KC) { return KC <= 16 ? 2 : 1; }
+__host__ __device__ constexpr int mq_tiles(int KC) { return KC <= 16 ? KNN_MQ_T : 1; }
 __host__ __device__ constexpr int mq_qpb(int KC) { return 16 * mq_tiles(KC) * MQ_W; }  // queries per workgroup
-static constexpr int MQ_TR = 256;                      // reference rows per LDS tile
+static constexpr int MQ_TR = KNN_MQ_TR;                // reference rows per LDS tile
 __host__ __device__ constexpr int mq_stride(int DP) { return DP + 4; }  // conflict-free 16-B reads
 typedef float mq_f4 __attribute__((ext_vector_type(4)));
 template <int DP, int KC>
