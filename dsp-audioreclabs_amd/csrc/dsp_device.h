@@ -263,7 +263,9 @@ __device__ __forceinline__ float canon_xval(int k, const CanonX &c)
 {
     return c.near0 ? (float)k + c.xa : ((float)k + c.xa) + c.xb;
 }
-// x of a sample pair, packed (v_pk_add_f32): the same bits as canon_xval per sample
+// x of a sample pair, packed (v_pk_add_f32): the same bits as canon_xval per sample (with
+// NEAR0 = false on a near0 clip, xb = +0 and fl(k + xa) + 0 = fl(k + xa): a zero sum is +0 in
+// round-to-nearest, so the bits are those of NEAR0 = true)
 template <bool NEAR0>
 __device__ __forceinline__ float2v canon_x2(int k0, int k1, const CanonX &c)
 {

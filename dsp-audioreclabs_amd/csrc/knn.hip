@@ -185,7 +185,7 @@ __global__ __launch_bounds__(KNN_TQ) void knn_screen(const float *__restrict__ r
 // infinite |r|^2 (distance +inf); the query's own row (self_offset) is masked only in the steps
 // that can hold one of the wave's 32 own rows.
 #ifndef KNN_MQ_W
-#define KNN_MQ_W 2
+#define KNN_MQ_W 4
 #endif
 #ifndef KNN_MQ_T
 #define KNN_MQ_T 2
