@@ -79,9 +79,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the multi-rank path on a one-GPU box (not a measurement): DSP_BENCH_ONE_DEVICE=1
+    # puts every rank on cuda:0 and DSP_BENCH_BACKEND=gloo replaces RCCL, which needs one GPU per rank
+    if os.environ.get("DSP_BENCH_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("DSP_BENCH_BACKEND", "nccl")
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
