@@ -137,6 +137,13 @@ _ERRORS = {
 }
 
 
+def _len_bucket(n, cap):
+    """n rounded up to 1/8-octave steps; not past the fused plan's cap when n itself fits it."""
+    step = 1 << max(0, int(n).bit_length() - 3)
+    m = -(-int(n) // step) * step
+    return min(m, cap) if n <= cap else m
+
+
 def process_audio_file(filepath, frame_length, frame_shift,
                        window_type='hamming',
                        do_endpoint_detection=True,
@@ -168,7 +175,10 @@ def process_pcm(pcm, sample_rate, frame_length, frame_shift, window_type='hammin
         raise ValueError(_ERRORS[_hip.CLIP_EMPTY])
     fx = _extractor(int(frame_length), int(frame_shift), window_type, do_endpoint_detection,
                     float(energy_high_ratio), float(energy_low_ratio), float(zcr_threshold_ratio))
-    out = {k: v.cpu().numpy() for k, v in fx(pcm.reshape(1, -1)).items()}
+    # the launch is sized for a length bucket (1/8 octave, clamped to the fused kernel's plan), so
+    # a caller looping over files of similar lengths, as the reference's experiments do
+    # (experiments/run_experiments.py:82-111), reuses one set of device output buffers
+    out = {k: v.cpu().numpy() for k, v in fx(pcm.reshape(1, -1), max_len=_len_bucket(n, fx.fused_cap())).items()}
     st = int(out["status"][0]) & 0xFF
     if st:
         raise ValueError(_ERRORS.get(st, "clip rejected by the device path (status %d)" % st))

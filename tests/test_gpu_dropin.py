@@ -59,6 +59,27 @@ def test_process_audio_file_and_features(tmp_path, vad):
         assert rel_ok((fr ** 2).sum(axis=1), r["seq"][:, 0])
 
 
+def test_file_loop_reuses_device_buffers(tmp_path):
+    """The reference's per-file loop (experiments/run_experiments.py:82-111): files of different
+    lengths within one length bucket share one set of device outputs, and each result still
+    equals the oracle's."""
+    from src import audio_processing as AP
+    from src.pipeline import create_window
+    from src.synth import make_clip
+    L, S = 1102, 441
+    fx = AP._extractor(L, S, "hamming", True, 0.5, 0.1, 1.5)
+    seen = set()
+    for i, n in enumerate([41000, 43217, 44100, 42001, 44099]):  # one bucket: (40960, 49152]
+        x = make_clip(300 + i)[:n]
+        p = tmp_path / ("f%d.wav" % i)
+        _write_wav(p, x)
+        _, _, md = AP.process_audio_file(str(p), L, S)
+        r = oracle.process_clip(x, L, S, create_window("hamming", L))
+        assert (md["start_point"], md["end_point"], md["n_frames"]) == (r["start"], r["end"], r["n_frames"])
+        seen.add(id(fx._bufs[next(iter(fx._bufs))]["feat"]))
+    assert len(seen) == 1
+
+
 def test_wav_formats_and_errors(tmp_path):
     from src.audio_processing import process_audio_file
     from src.pipeline import create_window
