@@ -184,6 +184,9 @@ __global__ __launch_bounds__(KNN_TQ) void knn_screen(const float *__restrict__ r
 // of the union -- and inserts only when some lane has a distance below it.  Padding rows carry an
 // infinite |r|^2 (distance +inf); the query's own row (self_offset) is masked only in the steps
 // that can hold one of the wave's 32 own rows.
+#ifndef KNN_MFMA_KC6
+#define KNN_MFMA_KC6 1
+#endif
 #ifndef KNN_MQ_W
 #define KNN_MQ_W 4
 #endif
@@ -781,10 +784,19 @@ KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
     l.exp = !l.hd && D < l.DP;
     l.KC = pick_kc(k);
     l.mfma = l.exp;  // every expanded-form screen runs on the matrix cores
+
     l.nsplit = l.mfma ? pick_nsplit_mfma(Nr, Nq, dsp::mq_qpb(l.KC), device_cus())
                       : pick_nsplit(Nr, Nq, l.hd ? dsp::KNN_TQ : dsp::KNN_TQ * dsp::KNN_QP);
 #ifdef DSP_KNN_DIAG  // diagnostic build only: forced split count (tools/knn_split_sweep.sh)
     if (const char *e = getenv("DSP_KNN_NSPLIT")) l.nsplit = std::max(1, std::min(64, atoi(e)));
+#endif
+#if KNN_MFMA_KC6
+    // matrix-core screen over short splits (<= 32k rows), k <= 5: six candidates per split
+    // (slack 1 instead of 3).  A short split's cost is mostly its list warm-up, and a shorter list
+    // inserts less often and more cheaply (12.5k x 100k, 5 splits of 20k rows: 1.19 -> 1.05 ms);
+    // over long splits the longer list measured faster (100k x 100k, 2 splits of 50k rows: 5.58
+    // against 6.06 ms) and stays.  Same tiles per wave (mq_tiles): the split count is unchanged.
+    if (l.mfma && k <= 5 && (Nr + l.nsplit - 1) / l.nsplit <= 32768) l.KC = 6;
 #endif
     size_t o = 0;
     l.ref32 = o; o += al((size_t)Nr * l.DP * 4);
@@ -903,6 +915,9 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
                        l.nsplit, cd, ci)
         DSP_SCREEN_MQ(16, 8); DSP_SCREEN_MQ(16, 16); DSP_SCREEN_MQ(16, 24); DSP_SCREEN_MQ(16, 36);
         DSP_SCREEN_MQ(32, 8); DSP_SCREEN_MQ(32, 16); DSP_SCREEN_MQ(32, 24); DSP_SCREEN_MQ(32, 36);
+#if KNN_MFMA_KC6
+        DSP_SCREEN_MQ(16, 6); DSP_SCREEN_MQ(32, 6);
+#endif
 #undef DSP_SCREEN_MQ
     } else {
         const dim3 g((unsigned)((Nq + dsp::KNN_TQ * dsp::KNN_QP - 1) / (dsp::KNN_TQ * dsp::KNN_QP)), (unsigned)l.nsplit);
@@ -917,6 +932,9 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
     knn_err_coeffs(l, D, er, ea);
     const int32_t *lbl = pred ? ref_labels : nullptr;
     switch (l.KC) {
+#if KNN_MFMA_KC6
+    case 6: launch_merge<6>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
+#endif
     case 8: launch_merge<8>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
     case 16: launch_merge<16>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
     case 24: launch_merge<24>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
