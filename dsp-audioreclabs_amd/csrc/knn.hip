@@ -203,6 +203,18 @@ __host__ __device__ constexpr int mq_qpb(int KC) { return 16 * mq_tiles(KC) * MQ
 static constexpr int MQ_TR = KNN_MQ_TR;                // reference rows per LDS tile
 __host__ __device__ constexpr int mq_stride(int DP) { return DP + 4; }  // conflict-free 16-B reads
 typedef float mq_f4 __attribute__((ext_vector_type(4)));
+// the value of lane ^ 16 / lane ^ 32 by the gfx950 permlane swaps (VALU, no LDS crossbar; the same
+// selection as dsp_device.h's shfl_xor_k, checked by tools/ubench/perm_check.hip)
+__device__ __forceinline__ float lane_xor_f(float v, int m, int lane)
+{
+    const int x = __float_as_int(v);
+    if (m == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return __int_as_float((lane & 16) ? r[0] : r[1]);
+    }
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return __int_as_float((lane & 32) ? r[0] : r[1]);
+}
 template <int DP, int KC>
 __global__ __launch_bounds__(64 * MQ_W) void knn_screen_mfma(const float *__restrict__ ref32, int64_t Nr,
                                                            const float *__restrict__ q32, int64_t Nq,
@@ -293,8 +305,8 @@ __global__ __launch_bounds__(64 * MQ_W) void knn_screen_mfma(const float *__rest
                     for (int v = 0; v < 4; v++)
                         if (c[v]) topk_insert<KC>(dl[t], il[t], acc[t][v], (int)(rb + 4 * rg + v));
                     float th = dl[t][KC - 1];
-                    th = fminf(th, __shfl_xor(th, 16, 64));
-                    th = fminf(th, __shfl_xor(th, 32, 64));
+                    th = fminf(th, lane_xor_f(th, 16, lane));
+                    th = fminf(th, lane_xor_f(th, 32, lane));
                     tau[t] = th;
                 }
             }
