@@ -14,11 +14,20 @@ Beside the metric (not part of ``value``):
   * ``window_sweep`` -- configs[2]: 10 000 clips x {rectangular, hamming, hanning};
   * ``allgather`` (N > 1) -- the one exchange step, all per-clip results in one RCCL all-gather;
   * ``knn`` -- configs[4]: exact k=5 self-query over 100 000 15-d vectors, queries sharded;
+  * ``configs0`` -- configs[0]'s frame sizes (Hamming, 1024 / 512 samples) on the same clips,
+    GPU frames/s beside its own CPU baseline (N = 1);
+  * ``configs1`` -- configs[1]: 1 000 clips, one launch (the latency-dominated small batch);
   * ``cpu_baseline`` (N = 1) -- the C restatement of the reference on this box's host cores,
     on a bounded sample of the same clips, whose outputs are also compared with the GPU's.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Without a launcher (no WORLD_SIZE in the environment) ``--gpus N`` > 1 starts the N ranks itself,
+as a child torch.distributed.run, before anything touches the GPU; under a launcher WORLD_SIZE must
+equal --gpus.  DSP_BENCH_ONE_DEVICE=1 (every rank on cuda:0) with DSP_BENCH_BACKEND=gloo rehearses
+the multi-rank path on a one-GPU box: the line then says ``rehearsal``, the backend and the number
+of physical GPUs, and is not a scaling measurement.
 """
 import argparse
 import json
@@ -56,7 +65,45 @@ def parse():
     ap.add_argument("--knn-ref", type=int, default=100000,
                     help="KNN leg (BASELINE configs[4]): reference rows, all of them queried (0: skip)")
     ap.add_argument("--knn-k", type=int, default=5)
+    ap.add_argument("--small-clips", type=int, default=1000, help="configs[1] leg: clips of one launch (0: skip)")
+    ap.add_argument("--cfg0", action=argparse.BooleanOptionalAction, default=True,
+                    help="configs[0] leg: 1024 / 512-sample frames")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="start the ranks and report the world size the process group saw (no GPU work)")
     return ap.parse_args()
+
+
+def free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(args):
+    """--gpus N > 1 without a launcher: run this script under torch.distributed.run with N ranks
+    (a child process; this one has not touched the GPU) and exit with its status."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
+def check_launch(args, world, rank, backend):
+    """--check-launch: the rank count the process group saw, without GPU work (CPU-testable)."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo" if backend != "nccl" else "nccl")
+        seen = dist.get_world_size()
+        dist.barrier()
+    else:
+        seen = 1
+    if rank == 0:
+        print(json.dumps({"check_launch": True, "gpus_flag": args.gpus, "world_size_env": world,
+                          "ranks_seen": seen, "backend": backend if world > 1 else None}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
 
 
 def timed_launches(fn, n, stream):
@@ -73,23 +120,36 @@ def timed_launches(fn, n, stream):
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args)  # before any GPU call
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus), file=sys.stderr)
+        return 2
     # rehearsal of the multi-rank path on a one-GPU box (not a measurement): DSP_BENCH_ONE_DEVICE=1
     # puts every rank on cuda:0 and DSP_BENCH_BACKEND=gloo replaces RCCL, which needs one GPU per rank
-    if os.environ.get("DSP_BENCH_ONE_DEVICE") == "1":
+    rehearsal = os.environ.get("DSP_BENCH_ONE_DEVICE") == "1"
+    if rehearsal:
         local = 0
     backend = os.environ.get("DSP_BENCH_BACKEND", "nccl")
+    if args.check_launch:
+        return check_launch(args, world, rank, backend)
+    import torch
+    import torch.distributed as dist
+
     if world > 1:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+    ranks_seen = dist.get_world_size() if world > 1 else 1
+    if ranks_seen != world:
+        print("bench.py: process group has %d ranks, WORLD_SIZE %d" % (ranks_seen, world), file=sys.stderr)
+        return 2
+    backend_name = ("RCCL" if backend == "nccl" else backend) if world > 1 else None
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
@@ -176,10 +236,13 @@ def main():
             torch.cuda.synchronize(dev)
             ts.append(time.perf_counter() - g0)
         ag = {"ms": round(float(np.median(ts)) * 1e3, 4), "bytes": args.clips * OUT_BYTES_PER_CLIP,
-              "collectives": 1, "what": "feat/start_end/n_frames/status of all clips, packed, RCCL all_gather"}
+              "collectives": 1, "backend": backend_name,
+              "what": "feat/start_end/n_frames/status of all clips, packed, one %s all_gather" % backend_name}
 
     sweep = window_sweep(args, fx, pool[0], dev, world, rank) if args.sweep_clips > 0 else None
-    knn = knn_leg(args, dev, world) if args.knn_ref > 0 else None
+    cfg0 = configs0_leg(args, pool[0], dev, world) if args.cfg0 else None
+    cfg1 = configs1_leg(args, fx, pool[0], dev, world) if args.small_clips > 0 else None
+    knn = knn_leg(args, dev, world, rank) if args.knn_ref > 0 else None
 
     result = None
     if rank == 0:
@@ -203,6 +266,7 @@ def main():
             "value": round(total_frames / elapsed, 1),
             "unit": "frames/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
             "steps": K,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / K * 1e3, 5),
@@ -222,18 +286,33 @@ def main():
                        "launch": "hip graph of the %d steps" % K if not args.no_graph else "python loop"},
             "roofline": roof,
         }
+        if rehearsal:
+            result["rehearsal"] = True
+            result["backend"] = backend_name
+            result["physical_gpus"] = 1
+            result["note"] = ("rehearsal of the multi-rank code path: %d ranks share cuda:0 over %s; not a "
+                              "scaling measurement" % (world, backend_name))
+        elif world > 1:
+            result["backend"] = backend_name
         if ag is not None:
             result["allgather"] = ag
+        if cfg0 is not None:
+            result["configs0"] = cfg0
+        if cfg1 is not None:
+            result["configs1"] = cfg1
         if sweep is not None:
             result["window_sweep"] = sweep
         if knn is not None:
             result["knn"] = knn
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(fx, pool[0], L, S, args.window, vad, args.cpu_seconds)
+            if cfg0 is not None:
+                fx0 = FeatureExtractor(1024, 512, "hamming", True, device=dev)
+                cfg0["cpu_baseline"] = cpu_baseline(fx0, pool[0], 1024, 512, "hamming", True, args.cpu_seconds / 2)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    return result
+    return 0
 
 
 def window_sweep(args, fx0, batch, dev, world, rank):
@@ -267,7 +346,56 @@ def window_sweep(args, fx0, batch, dev, world, rank):
             "windows": res}
 
 
-def knn_leg(args, dev, world):
+def configs0_leg(args, batch, dev, world):
+    """BASELINE configs[0]'s frame sizes (run.py --experiment classifier with Hamming frames of
+    1024 / 512 samples, /root/reference/config.py:35-40) on the rank's resident clips: GPU
+    frames/s (VAD frames + feature frames) from HIP-event launch times."""
+    import torch
+    import torch.distributed as dist
+    from src.pipeline import FeatureExtractor
+    fx = FeatureExtractor(1024, 512, "hamming", True, device=dev)
+    out = fx(batch)
+    assert not (out["status"].cpu().numpy() & 0xFF).any()
+    n, N = batch.shape
+    fr = out["n_frames"].to(torch.int64).sum().item() + ((N - 1024) // 512 + 1) * n
+    ms = timed_launches(lambda: fx(batch), 5, torch.cuda.current_stream(dev))
+    t = torch.tensor([ms, fr], dtype=torch.float64, device=dev)
+    if world > 1:
+        tm = t.clone()
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        ms, fr = tm[0].item(), t[1].item()
+    byts = n * world * (2 * N + OUT_BYTES_PER_CLIP)
+    return {"config": "BASELINE configs[0] frame sizes: Hamming, frame_length 1024, frame_shift 512 samples, "
+                      "VAD on; %d x 1 s clips" % (n * world),
+            "frames_per_s": round(fr / (ms * 1e-3), 1), "kernel_ms": round(ms, 4),
+            "hbm_frac": round(byts / (ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4)}
+
+
+def configs1_leg(args, fx, batch, dev, world):
+    """BASELINE configs[1]: 1 000 synthetic 1 s clips (Hamming, all features + VAD) in ONE launch
+    on one GPU -- a latency-dominated batch (about 2 clips per workgroup).  Reported per launch:
+    the kernel time (HIP events) and the host wall time of a synchronised call."""
+    import torch
+    n = min(args.small_clips, batch.shape[0])
+    sub = batch[:n]
+    out = fx(sub)
+    assert not (out["status"].cpu().numpy() & 0xFF).any()
+    fr = out["n_frames"].to(torch.int64).sum().item() + ((sub.shape[1] - fx.L) // fx.S + 1) * n
+    ms = timed_launches(lambda: fx(sub), 20, torch.cuda.current_stream(dev))
+    walls = []
+    for _ in range(20):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        fx(sub)
+        torch.cuda.synchronize(dev)
+        walls.append(time.perf_counter() - t0)
+    return {"config": "BASELINE configs[1]: %d x 1 s clips, one launch, Hamming, E/M/ZCR + VAD (rank 0)" % n,
+            "kernel_ms": round(ms, 4), "wall_ms_per_call": round(float(np.median(walls)) * 1e3, 4),
+            "frames_per_s_kernel": round(fr / (ms * 1e-3), 1)}
+
+
+def knn_leg(args, dev, world, rank):
     """BASELINE configs[4] beside the headline metric: exact k-NN (KNeighborsClassifier
     semantics) of every one of --knn-ref synthetic z-scored 15-d vectors against all of them
     (self excluded), queries sharded over the ranks, results gathered (one RCCL all-gather).
@@ -305,13 +433,40 @@ def knn_leg(args, dev, world):
         t = tt.item()
     pairs = float(n) * n
     tf = pairs * 45 / t / 1e12
-    return {"metric": "k-NN pairs/s (15-d, exact, k=%d, self-query, gathered)" % args.knn_k,
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        # the C oracle (sklearn semantics, fp64) on a bounded sample of the same queries, timed on
+        # the host cores; the GPU's answers for those queries must equal it bit for bit
+        idx, dist_, pred = knn_sharded(knn_classify, Xd, yd, Xd, args.knn_k, self_query=True)
+        cpu = knn_cpu_baseline(X, y, args.knn_k, idx, dist_, pred)
+    res = {"metric": "k-NN pairs/s (15-d, exact, k=%d, self-query, gathered)" % args.knn_k,
             "value": round(pairs / t, 1), "unit": "pairs/s", "ms": round(t * 1e3, 4),
             "ref": n, "queries": n, "queries_per_rank": -(-n // world),
             "roofline": {"bound": "mfma-f32", "achieved": round(tf, 2), "peak": 157.3 * world, "unit": "TFLOP/s",
                          "frac": round(tf / (157.3 * world), 4), "flop_per_pair": 45,
                          "note": "whole-job wall time incl. conversion, merge and the result all-gather"},
             "data": "synthetic z-scored 15-d vectors around 10 class centres"}
+    if cpu is not None:
+        res["cpu_baseline"] = cpu
+    return res
+
+
+def knn_cpu_baseline(X, y, k, idx, dist, pred, nq=1000):
+    """oracle.knn (a C restatement of KNeighborsClassifier's exact search + vote) over the first
+    nq self-queries on this box's host cores; parity of the GPU's answers on those queries."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    threads, _, _ = host_cores()
+    t0 = time.perf_counter()
+    i0, d0, p0 = oracle.knn(X, y, X[:nq], k, n_classes=10, self_offset=0, nthreads=threads)
+    dt = time.perf_counter() - t0
+    ok_i = bool(np.array_equal(idx[:nq].cpu().numpy(), i0))
+    ok_d = bool(np.array_equal(dist[:nq].cpu().numpy(), d0))
+    ok_p = bool(np.array_equal(pred[:nq].cpu().numpy(), p0))
+    return {"value": round(nq * X.shape[0] / dt, 1), "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": "%d self-queries x %d reference rows, C oracle (exact fp64 brute force, sklearn "
+                      "semantics), %d threads" % (nq, X.shape[0], threads),
+            "parity_on_sample": {"queries": nq, "idx_exact": ok_i, "dist_exact": ok_d, "pred_exact": ok_p}}
 
 
 def host_cores():
@@ -379,4 +534,4 @@ def cpu_baseline(fx, batch, L, S, window, vad, budget_s):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

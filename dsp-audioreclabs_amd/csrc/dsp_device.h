@@ -460,6 +460,17 @@ __device__ __forceinline__ unsigned long long shfl_xor_k(unsigned long long v, i
     const unsigned lo = shfl_xor_k((unsigned)v, m, lane), hi = shfl_xor_k((unsigned)(v >> 32), m, lane);
     return ((unsigned long long)hi << 32) | lo;
 }
+// lane ^ m for m = 16 or 32 by the gfx950 permlane swaps (no LDS crossbar; tools/ubench/perm_check.hip)
+__device__ __forceinline__ float lane_xor_f(float v, int m, int lane)
+{
+    const int x = __float_as_int(v);
+    if (m == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return __int_as_float((lane & 16) ? r[0] : r[1]);
+    }
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return __int_as_float((lane & 32) ? r[0] : r[1]);
+}
 template <int NH, typename K>
 __device__ __forceinline__ void wave_bitonic(K (&a)[NH], int lane)
 {

@@ -209,10 +209,12 @@ __device__ __forceinline__ void general_clip(const Params &p, Sh &s, const Ws &w
 {
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t o0 = p.offsets[i], nn = p.offsets[i + 1] - o0;
-    if (nn <= 0 && p.min_len == 0) {  // np.max of an empty array raises (:72)
+    // min_len == 0: this launch owns every clip, so an empty one (np.max of an empty array raises,
+    // :72) and one longer than max_len are reported here; otherwise they belong to another launch
+    if (p.min_len == 0 && (nn <= 0 || nn > p.max_len)) {
         if (tid < 15) p.feat[(int64_t)i * 15 + tid] = __builtin_nanf("");
         if (tid == 0) {
-            p.status[i] = DSP_CLIP_EMPTY;
+            p.status[i] = nn <= 0 ? DSP_CLIP_EMPTY : DSP_CLIP_TOO_LONG;
             p.start_end[2 * i] = p.start_end[2 * i + 1] = 0;
             p.n_frames[i] = 0;
         }

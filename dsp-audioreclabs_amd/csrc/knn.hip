@@ -27,6 +27,7 @@
 #include <algorithm>
 
 #include "dsp_audiorec.h"
+#include "dsp_device.h"
 
 namespace dsp {
 
@@ -203,18 +204,7 @@ __host__ __device__ constexpr int mq_qpb(int KC) { return 16 * mq_tiles(KC) * MQ
 static constexpr int MQ_TR = KNN_MQ_TR;                // reference rows per LDS tile
 __host__ __device__ constexpr int mq_stride(int DP) { return DP + 4; }  // conflict-free 16-B reads
 typedef float mq_f4 __attribute__((ext_vector_type(4)));
-// the value of lane ^ 16 / lane ^ 32 by the gfx950 permlane swaps (VALU, no LDS crossbar; the same
-// selection as dsp_device.h's shfl_xor_k, checked by tools/ubench/perm_check.hip)
-__device__ __forceinline__ float lane_xor_f(float v, int m, int lane)
-{
-    const int x = __float_as_int(v);
-    if (m == 16) {
-        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-        return __int_as_float((lane & 16) ? r[0] : r[1]);
-    }
-    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-    return __int_as_float((lane & 32) ? r[0] : r[1]);
-}
+// lane_xor_f (dsp_device.h): the value of lane ^ 16 / lane ^ 32 by the gfx950 permlane swaps
 template <int DP, int KC>
 __global__ __launch_bounds__(64 * MQ_W) void knn_screen_mfma(const float *__restrict__ ref32, int64_t Nr,
                                                            const float *__restrict__ q32, int64_t Nq,
@@ -828,26 +818,34 @@ void launch_screen(dim3 g, hipStream_t s, const float *r, int64_t Nr, const floa
                        self, nsplit, cd, ci);
 }
 
+// returns false when no merge kernel covers (KC, k): the layout broke KC >= k + KNN_SLACK
 template <int KC>
-void launch_merge(hipStream_t s, const double *ref, const double *query, int64_t Nr, int64_t Nq, int D, int k,
+bool launch_merge(hipStream_t s, const double *ref, const double *query, int64_t Nr, int64_t Nq, int D, int k,
                   int nsplit, int64_t self, const float *cd, const int *ci, const unsigned *mx, double er,
                   double ea, const int32_t *lbl, int32_t *idx, double *dist, int32_t *pred, int *fbc, int *fbl)
 {
     // 64-thread workgroups: 12 500 queries (one rank of the 8-GPU self-query) are 196 of them
     const dim3 g((unsigned)((Nq + 63) / 64)), b(64);
     // KC >= k + KNN_SLACK, so KC = 8 implies k <= 8 and KC = 16 implies k <= 16
+    if (k > KC) return false;
     if (k <= 8) {
         hipLaunchKernelGGL((dsp::knn_merge<KC, 8>), g, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self, cd, ci, mx,
                            er, ea, lbl, idx, dist, pred, fbc, fbl);
-    } else if (k <= 16) {
-        if constexpr (KC >= 16)
+        return true;
+    }
+    if constexpr (KC >= 16) {
+        if (k <= 16) {
             hipLaunchKernelGGL((dsp::knn_merge<KC, 16>), g, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self, cd, ci,
                                mx, er, ea, lbl, idx, dist, pred, fbc, fbl);
-    } else {
-        if constexpr (KC >= 24)
-            hipLaunchKernelGGL((dsp::knn_merge<KC, 32>), g, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self, cd, ci,
-                               mx, er, ea, lbl, idx, dist, pred, fbc, fbl);
+            return true;
+        }
     }
+    if constexpr (KC >= 24) {
+        hipLaunchKernelGGL((dsp::knn_merge<KC, 32>), g, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self, cd, ci,
+                           mx, er, ea, lbl, idx, dist, pred, fbc, fbl);
+        return true;
+    }
+    return false;
 }
 
 // err(d) = er * d + ea * (|q|^2 + max |r|^2) bounds |fp32 screened - fp64| distance.
@@ -943,15 +941,17 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
     double er, ea;
     knn_err_coeffs(l, D, er, ea);
     const int32_t *lbl = pred ? ref_labels : nullptr;
+    bool merged = false;
     switch (l.KC) {
 #if KNN_MFMA_KC6
-    case 6: launch_merge<6>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
+    case 6: merged = launch_merge<6>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
 #endif
-    case 8: launch_merge<8>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
-    case 16: launch_merge<16>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
-    case 24: launch_merge<24>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
-    default: launch_merge<36>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
+    case 8: merged = launch_merge<8>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
+    case 16: merged = launch_merge<16>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
+    case 24: merged = launch_merge<24>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
+    default: merged = launch_merge<36>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
     }
+    if (!merged) return DSP_ERR_ARGS;  // unreachable while KC >= k + KNN_SLACK (knn_layout)
     const unsigned fbgrid = (unsigned)(Nq < 512 ? Nq : 512);
     hipLaunchKernelGGL(dsp::knn_fallback, dim3(fbgrid), dim3(dsp::FB_T), 0, s, ref, query, Nr, D,
                        k, self_offset, fbc, fbl, lbl, idx, dist, pred);

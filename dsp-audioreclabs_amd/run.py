@@ -31,14 +31,24 @@ def main(argv=None):
     import config
     from experiments.run_experiments import SpeechRecognitionExperiment
     global last_experiment
-    if args.frame_length is not None:
-        if args.frame_length < 1:
-            ap.error('--frame-length must be positive')
-        config.FRAME_LENGTH = args.frame_length
-    if args.frame_shift is not None:
-        if args.frame_shift < 1:
-            ap.error('--frame-shift must be positive')
-        config.FRAME_SHIFT = args.frame_shift
+    for name, v in (('--frame-length', args.frame_length), ('--frame-shift', args.frame_shift)):
+        if v is not None and v < 1:
+            ap.error('%s must be positive' % name)
+    # the frame sizes apply to this run only: config's module values are restored on return, so a
+    # later main() in the same process without the flags gets config.py's defaults again
+    saved = (config.FRAME_LENGTH, config.FRAME_SHIFT)
+    try:
+        if args.frame_length is not None:
+            config.FRAME_LENGTH = args.frame_length
+        if args.frame_shift is not None:
+            config.FRAME_SHIFT = args.frame_shift
+        return _run(args, config, SpeechRecognitionExperiment)
+    finally:
+        config.FRAME_LENGTH, config.FRAME_SHIFT = saved
+
+
+def _run(args, config, SpeechRecognitionExperiment):
+    global last_experiment
     data_dir = os.environ.get('SPEECH_DATA_DIR', config.DATA_DIR)
     if not os.path.isdir(data_dir):
         print("data directory not found: %s (use --data-dir)" % data_dir)
@@ -57,7 +67,6 @@ def main(argv=None):
               % args.experiment)
     print(out)
     return 0
-
 
 if __name__ == '__main__':
     sys.exit(main())

@@ -221,8 +221,9 @@ def zscore_apply(X, mean, std):
     d = _hip.require_device()
     X = _as_device(X, torch.float64, d)
     mean = _as_device(mean, torch.float64, d)
-    std = _as_device(torch.where(torch.as_tensor(std) == 0, 1.0, torch.as_tensor(std, dtype=torch.float64)),
-                     torch.float64, d)
+    # a private float64 copy: std may be a read-only (e.g. broadcast) numpy view
+    std = _as_device(std, torch.float64, d)
+    std = torch.where(std == 0, torch.ones_like(std), std)
     out = torch.empty_like(X)
     N, D = X.shape
     _hip.check(_hip.lib().dsp_zscore_apply(_hip.ptr(X), N, D, _hip.ptr(mean), _hip.ptr(std), _hip.ptr(out),

@@ -113,7 +113,8 @@ int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, int B, int6
  * pcm          int16 (sample_bytes 2) or int32 (sample_bytes 4) samples, clips at offsets[b].
  * clip_index   int32 [nclip] clip numbers b to process (device; NULL: b = 0 .. nclip-1).  Only
  *              clips with min_len < len <= max_len are processed (min_len = 0: every clip,
- *              empty ones reported DSP_CLIP_EMPTY); the outputs of the others are untouched, so
+ *              empty ones reported DSP_CLIP_EMPTY and ones longer than max_len
+ *              DSP_CLIP_TOO_LONG); with min_len > 0 the outputs of the others are untouched, so
  *              a batch can be split between the two entry points without a host round trip.
  * outputs      as dsp_extract_features, indexed by clip number b.
  * workspace    device scratch of dsp_extract_general_workspace_bytes(nclip, max_len, L, S).

@@ -208,12 +208,10 @@ def test_run_py_sample_count_frames(tmp_path):
         for j in range(4):
             _write_wav(d / ("x%d.wav" % j), make_clip(4100 + 10 * c + j, 40000 + 997 * j, label=c, n_classes=3))
     saved = (config.FRAME_LENGTH, config.FRAME_SHIFT)
-    try:
-        assert run.main(["--data-dir", str(tmp_path), "--results-dir", str(tmp_path / "r"), "--experiment",
-                         "classifier", "--frame-length", "1024", "--frame-shift", "512"]) == 0
-        assert (config.FRAME_LENGTH, config.FRAME_SHIFT) == (1024, 512)
-    finally:
-        config.FRAME_LENGTH, config.FRAME_SHIFT = saved
+    assert run.main(["--data-dir", str(tmp_path), "--results-dir", str(tmp_path / "r"), "--experiment",
+                     "classifier", "--frame-length", "1024", "--frame-shift", "512"]) == 0
+    # the flags apply to that run only: config.py's values are back for the next main()
+    assert (config.FRAME_LENGTH, config.FRAME_SHIFT) == saved
     exp = run.last_experiment
     files, _ = list_dataset(str(tmp_path))
     assert exp.X.shape == (len(files), 15)
