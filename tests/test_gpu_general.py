@@ -146,6 +146,33 @@ def test_int32_stereo_sums_vs_oracle():
         _check_clip(out, i, c, 1102, 441, "hamming")
 
 
+def test_clips_past_explicit_max_len_report_too_long():
+    """An explicit max_len caps the clips processed: on the general-only paths (an int32 batch, and
+    an int16 batch at a frame length the fused plan cannot hold) a longer clip reports
+    DSP_CLIP_TOO_LONG with NaN features instead of leaving its outputs unwritten."""
+    import torch
+    from src.pipeline import FeatureExtractor
+    from src.synth import make_clip
+    for dtype, L, S in ((np.int32, 1102, 441), (np.int16, 40000, 441)):
+        clips = [make_clip(900 + i, n).astype(dtype) for i, n in enumerate((30000, 200000, 44100))]
+        off = np.zeros(len(clips) + 1, np.int64)
+        off[1:] = np.cumsum([c.size for c in clips])
+        pcm = np.concatenate(clips + [np.zeros(8, dtype)])
+        fx = FeatureExtractor(L, S, "hamming", True)
+        if dtype == np.int16:
+            assert fx.fused_cap() == 0
+        for o in fx._outputs(len(clips), 50000).values():  # stale contents must not survive
+            o.fill_(7)
+        out = {k: v.cpu().numpy() for k, v in fx(torch.as_tensor(pcm).cuda(), off, max_len=50000).items()}
+        assert out["status"][1] & 0xFF == 4, out["status"]  # DSP_CLIP_TOO_LONG
+        assert np.isnan(out["feat"][1]).all()
+        assert out["n_frames"][1] == 0 and (out["start_end"][1] == 0).all()
+        assert (out["status"][[0, 2]] & 0xFF == 0).all()
+        if dtype == np.int32:
+            for i in (0, 2):
+                _check_clip(out, i, clips[i], L, S, "hamming")
+
+
 def test_s16_stereo_golden_through_process_audio_file(golden, tmp_path):
     """The reference-generated 16-bit stereo WAV (tests/golden: wav/s16_stereo_clip) through the
     drop-in process_audio_file: endpoints exact, 15-d vector within tolerance."""
