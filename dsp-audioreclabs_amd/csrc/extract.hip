@@ -85,9 +85,7 @@ static constexpr int NRV = 4 * RREG;       // 16-B vectors per thread in registe
     } while (0)
 #endif
 
-// The kernel's only argument.  clip_exact (out of line) reads it in place through the kernel's
-// kernarg-segment pointer: explicit arguments start at offset 0 of that segment, so the layout
-// must stay a plain aggregate passed by value as the FIRST and ONLY kernel parameter.
+// The kernels' only argument, a plain aggregate passed by value.
 struct ExtractParams {
     const int16_t *pcm;
     const int64_t *offsets;
@@ -111,7 +109,7 @@ struct ExtractParams {
 };
 
 static_assert(__is_standard_layout(ExtractParams) && __is_trivially_copyable(ExtractParams),
-              "ExtractParams is read in place from the kernarg segment (clip_exact)");
+              "ExtractParams is a plain kernel argument block");
 static_assert(sizeof(ExtractParams) <= 1024, "kernel argument block");
 
 // ------------------------------------------------------------------------------------------
@@ -121,7 +119,7 @@ struct Shared {
     double pa, pb;            // the two order statistics of the VAD energies around p90
     double noise_e, noise_z;  // VAD noise estimates (:189-195, :239-245)
     double oslo[3], oshi[3];  // order statistics (F-1)/2 and F/2 of E, M, ZCR (medians)
-    int n3, n1, n6, exact, j0, j1, ndefer, next;
+    int n3, n1, n6, exact, j0, j1, next;
 };
 static_assert(sizeof(Shared) <= EXTRACT_SHARED_BYTES, "grow EXTRACT_SHARED_BYTES");
 
@@ -165,7 +163,6 @@ struct Ctx {
     int *rank;  // rank scratch: nvcap or 3 * fcap ints
     int *pS1;   // partial-word moments at the two ends of each VAD frame (2 * nvcap)
     unsigned long long *pS2;
-    int *defer;
     int64_t total;
     int stamp_clip;  // clip index for the diagnostic stamps
 };
@@ -476,6 +473,390 @@ __device__ __forceinline__ void partial_moments(const short8 (&q)[4], int e0, in
     t2 += s2;
 }
 
+// values every lane holds alike (read from LDS, say): pinned to scalar registers
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float uni(float v)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ double uni(double v)
+{
+    const long long b = __builtin_bit_cast(long long, v);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((int)b), hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __builtin_bit_cast(double, (long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// R1 of one 32-sample buffer word w of a clip (lead, n, nword): exact moments (sum k, sum k^2) to
+// wS1[w] / wS2[w]; the thread's running sum K, min and max (packed int16 min / max for the
+// interior words, whose 32 samples are all the clip's)
+struct R1Acc {
+    int K, kmin, kmax;
+    short2v pmin, pmax;
+};
+__device__ __forceinline__ R1Acc r1_acc_init()
+{
+    R1Acc a;
+    a.K = 0;
+    a.kmin = 0x7fffffff;
+    a.kmax = -0x7fffffff - 1;
+    a.pmin = (short2v){32767, 32767};
+    a.pmax = (short2v){-32768, -32768};
+    return a;
+}
+__device__ __forceinline__ void r1_word(const short8 *q, int w, int nword, int lead, int n, R1Acc &a, int *wS1,
+                                        unsigned long long *wS2)
+{
+    int s1 = 0;
+    unsigned long long s2 = 0;
+    if (w > 0 && w < nword - 1) {  // all 32 samples are the clip's
+        const short2v ones = {1, 1};
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+                const short2v d = half_pair(q[k], h);
+                a.pmin = __builtin_elementwise_min(a.pmin, d);
+                a.pmax = __builtin_elementwise_max(a.pmax, d);
+                s1 = __builtin_amdgcn_sdot2(d, ones, s1, false);
+                s2 += (unsigned)sq2(d);  // <= 2^31: unsigned
+            }
+    } else {  // first / last word of the clip: real samples only
+#pragma unroll 1
+        for (int k = 0; k < 4; k++) {
+            const short8 v = k == 0 ? q[0] : k == 1 ? q[1] : k == 2 ? q[2] : q[3];
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const int u = 32 * w + 8 * k + e;
+                const int x = v[e];
+                if (u >= lead && u < lead + n) {
+                    s1 += x;
+                    s2 += (unsigned)(x * x);
+                    a.kmin = min(a.kmin, x);
+                    a.kmax = max(a.kmax, x);
+                }
+            }
+        }
+    }
+    wS1[w] = s1;
+    wS2[w] = s2;
+    a.K += s1;
+}
+// the wave's R1 partials -> sh->red_*[wid] (every lane of the wave active)
+__device__ __forceinline__ void r1_reduce(const R1Acc &a, Shared *sh, int wid, int lane)
+{
+    const int kmn = min(a.kmin, min((int)a.pmin.x, (int)a.pmin.y));
+    const int kmx = max(a.kmax, max((int)a.pmax.x, (int)a.pmax.y));
+    const long long ks = (long long)wave_sum(a.K);  // <= 64 threads' sums < 2^31
+    const int wmn = wave_min(kmn), wmx = wave_max(kmx);
+    if (lane == 0) {
+        sh->red_k[wid] = ks;
+        sh->red_a[wid] = wmn;
+        sh->red_b[wid] = wmx;
+    }
+}
+// R2 of one buffer word: bit b set <=> buffer sample 32w + b is the clip's and k >= tpos (positive
+// after preprocess).  Packed saturating k - tpos per sample pair, the sign bytes gathered by
+// v_perm, their top bits by a multiply (k < tpos), inverted.
+__device__ __forceinline__ uint32_t pos_byte(const short8 &val, short2v tt, bool tbig)
+{
+    if (tbig) return 0u;  // tpos > 32767: no int16 sample can be positive
+    const unsigned a0 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 0), tt));
+    const unsigned a1 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 1), tt));
+    const unsigned a2 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 2), tt));
+    const unsigned a3 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 3), tt));
+    const unsigned x01 = __builtin_amdgcn_perm(a1, a0, 0x07050301u) & 0x80808080u;
+    const unsigned x23 = __builtin_amdgcn_perm(a3, a2, 0x07050301u) & 0x80808080u;
+    return ~(((x01 * 0x00204081u) >> 28) | (((x23 * 0x00204081u) >> 28) << 4)) & 0xFFu;
+}
+__device__ __forceinline__ uint32_t pos_word(const short8 *q, int w, int nword, int lead, int n, int tpos)
+{
+    const bool tbig = tpos > 32767;
+    const short2v tt = {(short)(tbig ? 32767 : tpos), (short)(tbig ? 32767 : tpos)};
+    uint32_t P = pos_byte(q[0], tt, tbig) | (pos_byte(q[1], tt, tbig) << 8) | (pos_byte(q[2], tt, tbig) << 16) |
+                 (pos_byte(q[3], tt, tbig) << 24);
+    if (w == 0 || w == nword - 1) {  // real samples only
+        const int lo_ = min(max(lead - 32 * w, 0), 32), hi_ = min(max(lead + n - 32 * w, 0), 32);
+        const uint32_t mhi = hi_ >= 32 ? ~0u : ((1u << hi_) - 1u);
+        const uint32_t mlo = lo_ >= 32 ? 0u : ~((1u << lo_) - 1u);
+        P &= mhi & mlo;
+    }
+    return P;
+}
+
+// remove_dc / normalize_audio (:49-75) in sample units, computed redundantly by every thread from
+// the per-wave partial sums in sh->red_*: the reference's float64 mean of k/32768 is exact, so
+// m = fl(K/n) and the peak is max(fl(kmax - m), fl(m - kmin)); a sample is positive after
+// preprocess <=> k >= tpos.
+struct ClipStats {
+    double mq, Mp, invM2;
+    float invMf;
+    int tpos, t0, nv;
+};
+__device__ __forceinline__ ClipStats clip_stats(const Shared *sh, int n, int L, int S, int do_vad)
+{
+    long long Kt = 0;
+    int kmin = 0x7fffffff, kmax = -0x7fffffff - 1;
+#pragma unroll
+    for (int w = 0; w < NWAVE; w++) {
+        Kt += sh->red_k[w];
+        kmin = min(kmin, sh->red_a[w]);
+        kmax = max(kmax, sh->red_b[w]);
+    }
+    ClipStats s;
+    s.mq = uni((double)Kt / (double)n);
+    s.Mp = uni(fmax((double)kmax - s.mq, s.mq - (double)kmin));
+    s.tpos = uni((int)floor(s.mq) + 1);
+    s.t0 = uni((int)floor(s.mq + 0.5));
+    s.invMf = uni(s.Mp > 0.0 ? (float)(1.0 / s.Mp) : 0.0f);  // as dsp_extract_general (same bits)
+    s.invM2 = uni(s.Mp > 0.0 ? 1.0 / (s.Mp * s.Mp) : 0.0);   // endpoint energies (one rounding)
+    s.nv = (do_vad && n >= L) ? (n - L) / S + 1 : 0;
+    return s;
+}
+
+// p90 order statistics of the VAD energies (:198) by ONE wave, nv <= 128: bitonic sort of the high
+// halves of the order-preserving keys; the rank's element is the one holding that high half, or,
+// when several do, the one of the right rank among them by the full key -> c.sh->pa / pb
+__device__ __forceinline__ void p90_select_wave(const Ctx &c, int nv, int lane)
+{
+    const double vi = (double)(nv - 1) * 0.9;
+    int r0, r1;
+    if (vi >= (double)(nv - 1)) {
+        r0 = r1 = nv - 1;
+    } else {
+        r0 = (int)floor(vi);
+        r1 = r0 + 1;
+    }
+    const unsigned long long f0 = lane < nv ? dkey(c.vE[lane]) : ~0ull;
+    const unsigned long long f1 = lane + 64 < nv ? dkey(c.vE[lane + 64]) : ~0ull;
+    const unsigned h0 = (unsigned)(f0 >> 32), h1 = (unsigned)(f1 >> 32);
+    unsigned a[2] = {h0, h1};
+    wave_bitonic<2>(a, lane);
+    auto full_at = [&](int r) -> double {
+        const unsigned kh = sorted_at<2>(a, r);  // never the pad's ~0u: r < nv
+        const unsigned long long c0 = __ballot(h0 == kh), c1 = __ballot(h1 == kh);
+        if (__popcll(c0) + __popcll(c1) == 1)
+            return dkey_value(c0 ? lane_read(f0, __ffsll((long long)c0) - 1)
+                                 : lane_read(f1, __ffsll((long long)c1) - 1));
+        const int rr = r - (__popcll(__ballot(h0 < kh)) + __popcll(__ballot(h1 < kh)));
+        unsigned long long res = 0;
+        for (int hh = 0; hh < 2; hh++) {
+            unsigned long long cm = hh ? c1 : c0;
+            while (cm) {
+                const int l = __ffsll((long long)cm) - 1;
+                cm &= cm - 1;
+                const unsigned long long e = lane_read(hh ? f1 : f0, l);
+                const int lt = __popcll(__ballot(h0 == kh && f0 < e)) + __popcll(__ballot(h1 == kh && f1 < e));
+                const int eq = __popcll(__ballot(f0 == e)) + __popcll(__ballot(f1 == e));
+                if (rr >= lt && rr < lt + eq) res = e;
+            }
+        }
+        return dkey_value(res);
+    };
+    const double pa = full_at(r0), pb = full_at(r1);
+    if (lane == 0) {
+        c.sh->pa = pa;
+        c.sh->pb = pb;
+    }
+}
+
+// the partial word endpoint pass A needs for frame end t = tid (FAST layout: one frame end per
+// thread), issued early so that it is in flight across a barrier; past the range it reads zeros
+__device__ __forceinline__ int vad_partial_issue(const ExtractParams &p, const ClipRef &cur, int L, int S, int nv,
+                                                 int t, short8 (&qa)[4], int &e0, int &e1)
+{
+    const int pw = vad_partial_word(cur, L, S, nv, t, e0, e1);
+    const __amdgpu_buffer_rsrc_t rs = clip_rsrc(p, cur);
+    const int off = pw >= 0 ? 64 * pw : 0x40000000;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        qa[k] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * k, 0, 0));
+    return pw;
+}
+
+// VAD frames, FAST layout (nv <= 128 <= NT / 2): one lane pair per frame -- lane h of pair f owns
+// frame end t = 2f + h = tid (its partial word qa issued by vad_partial_issue), adds that word's
+// exact moments, and half of the interior word sums and of the sign changes; no pass-A barrier.
+// Frame f = buffer samples [u0, u0 + L): exact moments (wS1/wS2 words + the partial words at its
+// ends), sign changes from the positive bits -> c.vE / c.vZ.
+__device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur, int L, int S, const ClipStats &cs,
+                                                const short8 (&qa)[4], int pa_w, int pa_e0, int pa_e1, int tid)
+{
+    const int nv = cs.nv, lead = cur.lead;
+    const int f = tid >> 1, lh = tid & 1;
+    const bool act = f < nv;
+    int s1 = 0;
+    unsigned long long s2 = 0;
+    int zc = 0;
+    if (act) {
+        if (pa_w >= 0 && !(DSP_ABL & 8)) partial_moments(qa, pa_e0, pa_e1, s1, s2);
+        const int u0 = lead + f * S, u1 = u0 + L;
+        const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
+        const int wi0 = (u0 & 31) ? wa + 1 : wa, wi1 = (u1 & 31) ? wb - 1 : wb;
+        const int per = (wi1 - wi0 + 2) >> 1;
+        const int ws = wi0 + lh * per, we = min(ws + per - 1, wi1);
+#pragma unroll 4
+        for (int w = ws; w <= we; w++) {
+            s1 += c.wS1[w];
+            s2 += c.wS2[w];
+        }
+        const int np_ = L - 1, ph = (np_ + 1) >> 1;  // pairs [u0, u1 - 1) in halves
+        const int x0 = u0 + min(lh * ph, np_), x1 = u0 + min((lh + 1) * ph, np_);
+        zc = chg_run(c.posw, x0, x1);
+    }
+    s1 += dpp_i(s1, DPP_QXOR1);
+    {
+        const unsigned lo = dpp_i((int)(unsigned)s2, DPP_QXOR1), hi = dpp_i((int)(unsigned)(s2 >> 32), DPP_QXOR1);
+        s2 += ((unsigned long long)hi << 32) | lo;
+    }
+    zc += dpp_i(zc, DPP_QXOR1);
+    if (act && lh == 0) {
+        c.vE[f] = energy_from_moments(s2, s1, L, cs.t0, cs.mq - (double)cs.t0, cs.invM2);
+        c.vZ[f] = zc;
+    }
+}
+
+// R4: windowed frames over the crop [st, en) (:378, :299-333; fe.py:12-43) -> c.fE / fM / fZ.
+// One 16-lane row per frame (4 frames per wave), in the canonical order of dsp_device.h: the
+// frame's clip-relative 8-sample vectors are re-read from L2 (16-B loads at the clip's own 2-byte
+// alignment) and lane rl takes vectors va + rl + 16k, so the sums do not depend on where the clip
+// sits in the buffer and equal dsp_extract_general's.  Per sample y = w_j x (the reference's
+// windowed frame, :329-331), E += y^2, M += |y|; the weights of a vector's 8 samples are two
+// aligned 16-B reads from the window copy shifted by fs mod 4.  Frame group g of 4 frames goes to
+// the wave whose rank (wrank, 0 .. NWAVE-1) is g mod NWAVE.  Returns F.
+__device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int st, int en,
+                                         const ClipStats &cs, int j0, int j1, int wrank, int lane)
+{
+    const int L = p.L, S = p.S, n = cur.n, lead = cur.lead;
+    const int m = en - st;  // > 0 always (start < end)
+    const int F = (m <= L) ? 1 : (m - L + S - 1) / S + 1;
+    const float sE = cs.invMf * cs.invMf, sM = cs.invMf;
+    const int wrow = EXTRACT_WROW(L);
+    const CanonX cx = canon_x(cs.mq, cs.t0);
+    // a 16-B load ending past the clip's last buffer vector drops a dword that straddles the
+    // descriptor's end (range checks are per dword): with an odd lead and a clip ending on a
+    // vector boundary that dword holds the last sample, patched in from the aligned vector
+    const int vfix = ((lead & 1) && ((lead + n) & 7) == 0) ? (n - 1) >> 3 : -1;
+    const short klast = vfix >= 0 ? load_vec(p, cur, cur.nvec - 1)[7] : (short)0;
+    auto frame_vec = [&](auto padded_t, auto near_t, const short8 &x8, const float *wr, int jb, int lim,
+                         float2v &ea, float &m0, float &m1) {
+        constexpr bool PADDED = decltype(padded_t)::value, NEAR0 = decltype(near_t)::value;
+        const float4 wa = *reinterpret_cast<const float4 *>(wr + jb);
+        const float4 wb = *reinterpret_cast<const float4 *>(wr + jb + 4);
+        const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            float2v w = {wv[2 * h], wv[2 * h + 1]};
+            if (PADDED) {  // samples past the crop are zero padding
+                const int j = jb + 2 * h;  // window index of the pair's first sample
+                w.x = j < lim ? w.x : 0.f;
+                w.y = j + 1 < lim ? w.y : 0.f;
+            }
+            canon_pair(w, canon_x2<NEAR0>(x8[2 * h], x8[2 * h + 1], cx), ea, m0, m1);
+        }
+    };
+    constexpr int R4_KV = EXTRACT_R4_KV;  // vectors per lane in one batch
+    const int rl = lane & 15, row = lane >> 4;
+    for (int gi = wrank; !(DSP_ABL & 1) && 4 * gi < F; gi += NWAVE) {
+        const int g = 4 * gi + row;
+        const bool act = g < F;
+        const int gc = act ? g : F - 1;
+        const int fs = st + gc * S;
+        const int lim = min(L, en - fs);  // samples beyond the crop are zero padding
+        const bool padded = lim < L;
+        const int va = fs >> 3, vb = (fs + lim - 1) >> 3;
+        const int r = fs & 3;  // copy whose rows start at window index = -fs (mod 4)
+        const float *wr = c.wtab + r * wrow + EXTRACT_WPAD + r;  // wr[j] = w[j], j = -7 .. L + 7
+        float2v ea = {0.f, 0.f};
+        float m0 = 0.f, m1 = 0.f;
+        for (int v0 = va; v0 <= vb; v0 += 16 * R4_KV) {
+            short8 xv[R4_KV];
+#pragma unroll
+            for (int k = 0; k < R4_KV; k++) xv[k] = load_cvec(p, cur, v0 + rl + 16 * k);
+            if (vfix >= 0)  // clip-uniform, rare
+#pragma unroll
+                for (int k = 0; k < R4_KV; k++)
+                    if (v0 + rl + 16 * k == vfix) xv[k][(n - 1) & 7] = klast;
+            auto run = [&](auto pt, auto nt) {
+#pragma unroll
+                for (int k = 0; k < R4_KV; k++) {
+                    const int v = v0 + rl + 16 * k;
+                    if (v <= vb) frame_vec(pt, nt, xv[k], wr, 8 * v - fs, lim, ea, m0, m1);
+                }
+            };
+            if (padded)
+                cx.near0 ? run(BoolT<true>(), BoolT<true>()) : run(BoolT<true>(), BoolT<false>());
+            else if (cx.near0)
+                run(BoolT<false>(), BoolT<true>());
+            else
+                run(BoolT<false>(), BoolT<false>());
+        }
+        const float E1 = dpp_row_reduce(ea.x + ea.y, OpAdd()) * sE;
+        const float M1 = dpp_row_reduce(m0 + m1, OpAdd()) * sM;
+        // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in
+        // [j0, j1]) and j < lim; transitions into the window's zero ends / padding count too
+        const int ia = fs + j0, ib = min(fs + j1, en - 1);  // sample coords
+        int z = dpp_row_reduce(ia < ib ? chg_count(c.posw, ia + lead, ib + lead, rl, 16) : 0, OpAdd());
+        if (ia <= ib) {
+            if (j0 > 0) z += pos_bit(c.posw, ia + lead);
+            if (ib < fs + L - 1) z += pos_bit(c.posw, ib + lead);
+        }
+        if (act && rl == 0) {
+            c.fE[g] = E1;
+            c.fM[g] = M1;
+            c.fZ[g] = z;
+        }
+    }
+    return F;
+}
+
+// R5 for F <= 128 (compute_statistics x 3, fe.py:46-62): six jobs on waves 0..5 -- wave q (q < 3)
+// the median of sequence q (E, M, ZCR) by an in-wave bitonic sort, wave 3 + q its mean /
+// population std (fp64 sums) / max / min -- no barrier.  np.median: the middle order statistic
+// (odd F) or the mean of the two middle ones.
+__device__ __forceinline__ void r5_fast(const Ctx &c, int F, float *featb, int wid, int lane)
+{
+    const int r0 = (F - 1) / 2, r1 = F / 2;
+    for (int job = wid; !(DSP_ABL & 2) && job < 6; job += NWAVE) {
+        const int q = job % 3;
+        auto get = [&](int j) -> float { return q == 0 ? c.fE[j] : q == 1 ? c.fM[j] : (float)c.fZ[j]; };
+        const bool in0 = lane < F, in1 = lane + 64 < F;
+        const float x0 = in0 ? get(lane) : 0.f, x1 = in1 ? get(lane + 64) : 0.f;
+        if (job < 3) {  // median by an in-wave bitonic sort
+            unsigned a[2] = {in0 ? fkey(x0) : ~0u, in1 ? fkey(x1) : ~0u};
+            float v0, v1;
+            if (F <= 64) {
+                unsigned b[1] = {a[0]};
+                wave_bitonic<1>(b, lane);
+                v0 = fkey_value(sorted_at<1>(b, r0));
+                v1 = fkey_value(sorted_at<1>(b, r1));
+            } else {
+                wave_bitonic<2>(a, lane);
+                v0 = fkey_value(sorted_at<2>(a, r0));
+                v1 = fkey_value(sorted_at<2>(a, r1));
+            }
+            double med;
+            {
+#pragma clang fp contract(off)
+                med = (F & 1) ? (double)v1 : ((double)v0 + (double)v1) / 2.0;
+            }
+            if (lane == 0) featb[5 * q + 4] = (float)med;
+        }
+        if (job >= 3) {  // mean, population std (fp64 sums), max, min
+            const double s = wave_sum((in0 ? (double)x0 : 0.0) + (in1 ? (double)x1 : 0.0));
+            const float mx = wave_reduce(fmaxf(in0 ? x0 : -INFINITY, in1 ? x1 : -INFINITY), OpMax());
+            const float mn = wave_reduce(fminf(in0 ? x0 : INFINITY, in1 ? x1 : INFINITY), OpMin());
+            const double mean = s / (double)F;
+            const double d0 = in0 ? (double)x0 - mean : 0.0, d1 = in1 ? (double)x1 - mean : 0.0;
+            const double qq = wave_sum(fma(d0, d0, d1 * d1));
+            if (lane < 4) {
+                const double o = lane == 0 ? mean : lane == 1 ? sqrt(qq / (double)F) : lane == 2 ? (double)mx
+                                 : (double)mn;
+                featb[5 * q + lane] = (float)o;
+            }
+        }
+    }
+}
+
 // One clip, start to finish; its first RREG words are already in flight into regs (word
 // r * NT + tid in regs[4r .. 4r+3]).  EXACT = false: endpoint energies from exact moments,
 // decisions certified; returns false on a near tie (the clip is then redone with EXACT = true
@@ -502,45 +883,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
 #endif
 
     // ---- R1: integer sum / min / max; exact moments per 32-sample word -----------------------
-    int K = 0;  // <= RREG * 32 * 32768 per thread (longer clips: one word per loop trip)
-    int kmin_s = 0x7fffffff, kmax_s = -0x7fffffff - 1;
-    short2v pmin = {32767, 32767}, pmax = {-32768, -32768};
-    auto r1_word = [&](const short8 *q, int w) {
-        int s1 = 0;
-        unsigned long long s2 = 0;
-        if (w > 0 && w < nword - 1) {  // all 32 samples are the clip's
-            const short2v ones = {1, 1};
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-#pragma unroll
-                for (int h = 0; h < 4; h++) {
-                    const short2v d = half_pair(q[k], h);
-                    pmin = __builtin_elementwise_min(pmin, d);
-                    pmax = __builtin_elementwise_max(pmax, d);
-                    s1 = __builtin_amdgcn_sdot2(d, ones, s1, false);
-                    s2 += (unsigned)sq2(d);  // <= 2^31: unsigned
-                }
-        } else {  // first / last word of the clip: real samples only
-#pragma unroll 1
-            for (int k = 0; k < 4; k++) {
-                const short8 v = k == 0 ? q[0] : k == 1 ? q[1] : k == 2 ? q[2] : q[3];
-#pragma unroll
-                for (int e = 0; e < 8; e++) {
-                    const int u = 32 * w + 8 * k + e;
-                    const int x = v[e];
-                    if (u >= lead && u < lead + n) {
-                        s1 += x;
-                        s2 += (unsigned)(x * x);
-                        kmin_s = min(kmin_s, x);
-                        kmax_s = max(kmax_s, x);
-                    }
-                }
-            }
-        }
-        c.wS1[w] = s1;
-        c.wS2[w] = s2;
-        K += s1;
-    };
+    R1Acc acc = r1_acc_init();  // K <= RREG * 32 * 32768 per thread (longer clips: one word per trip)
     // clips of up to RREG * NT words stream from the registers loaded before this call; longer
     // ones are read word by word here and again in R2 (the second read hits L2)
     const bool inreg = FAST || nword <= RREG * NT;
@@ -548,89 +891,36 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
 #pragma unroll
         for (int r = 0; r < RREG; r++) {
             const int w = r * NT + tid;
-            if (w < nword) r1_word(&regs[4 * r], w);
+            if (w < nword) r1_word(&regs[4 * r], w, nword, lead, n, acc, c.wS1, c.wS2);
         }
     } else {
 #pragma unroll 1
         for (int w = tid; w < nword; w += NT) {
             short8 q[4];
             issue_word(q, p, cur, w);
-            r1_word(q, w);
+            r1_word(q, w, nword, lead, n, acc, c.wS1, c.wS2);
         }
     }
-    {
-        const int kmn = min(kmin_s, min((int)pmin.x, (int)pmin.y));
-        const int kmx = max(kmax_s, max((int)pmax.x, (int)pmax.y));
-        const long long ks = (long long)wave_sum(K);  // <= 64 threads' sums < 2^31
-        const int wmn = wave_min(kmn), wmx = wave_max(kmx);
-        if (lane == 0) {
-            sh->red_k[wid] = ks;
-            sh->red_a[wid] = wmn;
-            sh->red_b[wid] = wmx;
-        }
-    }
+    r1_reduce(acc, sh, wid, lane);
     __syncthreads();
-    // remove_dc / normalize_audio (:49-75) in sample units, computed redundantly by every thread:
-    // the reference's float64 mean of k/32768 is exact, so m = fl(K/n) and the peak is
-    // max(fl(kmax - m), fl(m - kmin)); a sample is positive after preprocess <=> k >= t.
-    long long Kt = 0;
-    int kmin = 0x7fffffff, kmax = -0x7fffffff - 1;
-#pragma unroll
-    for (int w = 0; w < NWAVE; w++) {
-        Kt += sh->red_k[w];
-        kmin = min(kmin, sh->red_a[w]);
-        kmax = max(kmax, sh->red_b[w]);
-    }
-    const double mq = (double)Kt / (double)n;
-    const double Mp = fmax((double)kmax - mq, mq - (double)kmin);
-    const int tpos = (int)floor(mq) + 1;
-    const int t0 = (int)floor(mq + 0.5);
-    const float invMf = Mp > 0.0 ? (float)(1.0 / Mp) : 0.0f;  // as dsp_extract_general (same bits)
-    const double invM2 = Mp > 0.0 ? 1.0 / (Mp * Mp) : 0.0;  // endpoint energies (one rounding)
-    const int nv = (p.do_vad && n >= L) ? (n - L) / S + 1 : 0;
+    const ClipStats cs = clip_stats(sh, n, L, S, p.do_vad);
+    const double mq = cs.mq, Mp = cs.Mp;
+    const int tpos = cs.tpos, t0 = cs.t0, nv = cs.nv;
     STAMP(i, 1);
 
     // ---- R2: positive-sample bits, one 32-bit word per 32 buffer samples ---------------------
-    const bool tbig = tpos > 32767;  // no int16 sample can be positive
-    const short2v tt = {(short)(tbig ? 32767 : tpos), (short)(tbig ? 32767 : tpos)};
-    auto pos_byte = [&](const short8 &val) -> uint32_t {
-        if (tbig) return 0u;
-        const unsigned a0 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 0), tt));
-        const unsigned a1 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 1), tt));
-        const unsigned a2 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 2), tt));
-        const unsigned a3 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 3), tt));
-        // the sign bytes of the four 16-bit results of each dword pair, then their top bits (k < t)
-        const unsigned x01 = __builtin_amdgcn_perm(a1, a0, 0x07050301u) & 0x80808080u;
-        const unsigned x23 = __builtin_amdgcn_perm(a3, a2, 0x07050301u) & 0x80808080u;
-        return ~(((x01 * 0x00204081u) >> 28) | (((x23 * 0x00204081u) >> 28) << 4)) & 0xFFu;
-    };
-    auto r2_word = [&](const short8 *q, int w) {
-        uint32_t P = pos_byte(q[0]) | (pos_byte(q[1]) << 8) | (pos_byte(q[2]) << 16) | (pos_byte(q[3]) << 24);
-        if (w == 0 || w == nword - 1) {  // real samples only
-            const int lo_ = min(max(lead - 32 * w, 0), 32), hi_ = min(max(lead + n - 32 * w, 0), 32);
-            const uint32_t mhi = hi_ >= 32 ? ~0u : ((1u << hi_) - 1u);
-            const uint32_t mlo = lo_ >= 32 ? 0u : ~((1u << lo_) - 1u);
-            P &= mhi & mlo;
-        }
-        c.posw[w] = P;
-    };
     if (inreg) {
 #pragma unroll
         for (int r = 0; r < RREG; r++) {
             const int w = r * NT + tid;
-            if (w < nword) {
-                if (DSP_ABL & 4)
-                    c.posw[w] = 0;
-                else
-                    r2_word(&regs[4 * r], w);
-            }
+            if (w < nword) c.posw[w] = (DSP_ABL & 4) ? 0u : pos_word(&regs[4 * r], w, nword, lead, n, tpos);
         }
     } else {
 #pragma unroll 1
         for (int w = tid; w < nword; w += NT) {
             short8 q[4];
             issue_word(q, p, cur, w);
-            r2_word(q, w);
+            c.posw[w] = pos_word(q, w, nword, lead, n, tpos);
         }
     }
     if (tid < 2) c.posw[nword + tid] = 0;
@@ -639,15 +929,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     short8 qa[4];
     int pa_w = -1, pa_e0 = 0, pa_e1 = 0;
     if constexpr (!EXACT) {
-        if constexpr (FAST) {
-            const int pw = vad_partial_word(cur, L, S, nv, tid, pa_e0, pa_e1);
-            const __amdgpu_buffer_rsrc_t rs = clip_rsrc(p, cur);
-            const int off = pw >= 0 ? 64 * pw : 0x40000000;  // past the range: reads zeros
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                qa[k] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * k, 0, 0));
-            pa_w = pw;
-        }
+        if constexpr (FAST) pa_w = vad_partial_issue(p, cur, L, S, nv, tid, qa, pa_e0, pa_e1);
     }
     __syncthreads();
     STAMP(i, 2);
@@ -660,40 +942,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
         // Pass A, one thread per frame end: the partial word's moments (FAST: loaded before the
         // next clip's prefetch; otherwise re-read from L2 here).
         if constexpr (FAST && !EXACT) {
-            // one lane pair per frame: lane h of pair f owns frame end t = 2f + h = tid (its
-            // partial word was loaded before the barrier), adds that word's exact moments, and
-            // half of the interior word sums and of the sign changes; no pass-A barrier
-            const int f = tid >> 1, lh = tid & 1;
-            const bool act = f < nv;
-            int s1 = 0;
-            unsigned long long s2 = 0;
-            int zc = 0;
-            if (act) {
-                if (pa_w >= 0 && !(DSP_ABL & 8)) partial_moments(qa, pa_e0, pa_e1, s1, s2);
-                const int u0 = lead + f * S, u1 = u0 + L;
-                const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
-                const int wi0 = (u0 & 31) ? wa + 1 : wa, wi1 = (u1 & 31) ? wb - 1 : wb;
-                const int per = (wi1 - wi0 + 2) >> 1;
-                const int ws = wi0 + lh * per, we = min(ws + per - 1, wi1);
-#pragma unroll 4
-                for (int w = ws; w <= we; w++) {
-                    s1 += c.wS1[w];
-                    s2 += c.wS2[w];
-                }
-                const int np_ = L - 1, ph = (np_ + 1) >> 1;  // pairs [u0, u1 - 1) in halves
-                const int x0 = u0 + min(lh * ph, np_), x1 = u0 + min((lh + 1) * ph, np_);
-                zc = chg_run(c.posw, x0, x1);
-            }
-            s1 += dpp_i(s1, DPP_QXOR1);
-            {
-                const unsigned lo = dpp_i((int)(unsigned)s2, DPP_QXOR1), hi = dpp_i((int)(unsigned)(s2 >> 32), DPP_QXOR1);
-                s2 += ((unsigned long long)hi << 32) | lo;
-            }
-            zc += dpp_i(zc, DPP_QXOR1);
-            if (act && lh == 0) {
-                c.vE[f] = energy_from_moments(s2, s1, L, t0, mq - (double)t0, invM2);
-                c.vZ[f] = zc;
-            }
+            vad_frames_fast(c, cur, L, S, cs, qa, pa_w, pa_e0, pa_e1, tid);
             STAMP(i, 7);
         } else {
             {
@@ -752,7 +1001,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                     if (act && lq == 0) {
                         if (!FAST) c.rank[f] = 0;
                         c.vE[f] = EXACT ? np_energy_exact(clip_g, f * S, L, mq, Mp)
-                                        : energy_from_moments(s2, s1, L, t0, mq - (double)t0, invM2);
+                                        : energy_from_moments(s2, s1, L, t0, mq - (double)t0, cs.invM2);
                         c.vZ[f] = zc;
                     }
                 }
@@ -780,37 +1029,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                         // it takes issue priority over the co-resident workgroup's waves until the
                         // decisions are made (2% at 100k clips)
                         __builtin_amdgcn_s_setprio(2);
-                        const unsigned long long f0 = lane < nv ? dkey(c.vE[lane]) : ~0ull;
-                        const unsigned long long f1 = lane + 64 < nv ? dkey(c.vE[lane + 64]) : ~0ull;
-                        const unsigned h0 = (unsigned)(f0 >> 32), h1 = (unsigned)(f1 >> 32);
-                        unsigned a[2] = {h0, h1};
-                        wave_bitonic<2>(a, lane);
-                        auto full_at = [&](int r) -> double {
-                            const unsigned kh = sorted_at<2>(a, r);  // never the pad's ~0u: r < nv
-                            const unsigned long long c0 = __ballot(h0 == kh), c1 = __ballot(h1 == kh);
-                            if (__popcll(c0) + __popcll(c1) == 1)
-                                return dkey_value(c0 ? lane_read(f0, __ffsll((long long)c0) - 1)
-                                                     : lane_read(f1, __ffsll((long long)c1) - 1));
-                            const int rr = r - (__popcll(__ballot(h0 < kh)) + __popcll(__ballot(h1 < kh)));
-                            unsigned long long res = 0;
-                            for (int hh = 0; hh < 2; hh++) {
-                                unsigned long long cm = hh ? c1 : c0;
-                                while (cm) {
-                                    const int l = __ffsll((long long)cm) - 1;
-                                    cm &= cm - 1;
-                                    const unsigned long long e = lane_read(hh ? f1 : f0, l);
-                                    const int lt = __popcll(__ballot(h0 == kh && f0 < e)) + __popcll(__ballot(h1 == kh && f1 < e));
-                                    const int eq = __popcll(__ballot(f0 == e)) + __popcll(__ballot(f1 == e));
-                                    if (rr >= lt && rr < lt + eq) res = e;
-                                }
-                            }
-                            return dkey_value(res);
-                        };
-                        const double pa = full_at(r0), pb = full_at(r1);
-                        if (lane == 0) {
-                            sh->pa = pa;
-                            sh->pb = pb;
-                        }
+                        p90_select_wave(c, nv, lane);
                     }
                 } else if (nv <= 256) {
                     ballot_select<double>([&](int j) { return c.vE[j]; }, nv, r0, r1, &sh->pa, &sh->pb, wid, lane);
@@ -849,95 +1068,8 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     }
     STAMP(i, 4);
 
-    // ---- R4: windowed frames over the crop [st, en) (:378, :299-333; fe.py:12-43) ---------
-    // One 16-lane row per frame (4 frames per wave), in the canonical order of dsp_device.h: the
-    // frame's clip-relative 8-sample vectors are re-read from L2 (16-B loads at the clip's own
-    // 2-byte alignment) and lane rl takes vectors va + rl + 16k, so the sums do not depend on where
-    // the clip sits in the buffer and equal dsp_extract_general's.  Per sample y = w_j x (the
-    // reference's windowed frame, :329-331), E += y^2, M += |y|; the weights of a vector's 8
-    // samples are two aligned 16-B reads from the window copy shifted by fs mod 4.
-    const int m = en - st;  // > 0 always (start < end)
-    const int F = (m <= L) ? 1 : (m - L + S - 1) / S + 1;
-    const int j0 = sh->j0, j1 = sh->j1;
-    const float sE = invMf * invMf, sM = invMf;
-    const int wrow = EXTRACT_WROW(L);
-    const CanonX cx = canon_x(mq, t0);
-    // a 16-B load ending past the clip's last buffer vector drops a dword that straddles the
-    // descriptor's end (range checks are per dword): with an odd lead and a clip ending on a
-    // vector boundary that dword holds the last sample, patched in from the aligned vector
-    const int vfix = ((lead & 1) && ((lead + n) & 7) == 0) ? (n - 1) >> 3 : -1;
-    const short klast = vfix >= 0 ? load_vec(p, cur, cur.nvec - 1)[7] : (short)0;
-    auto frame_vec = [&](auto padded_t, auto near_t, const short8 &x8, const float *wr, int jb, int lim,
-                         float2v &ea, float &m0, float &m1) {
-        constexpr bool PADDED = decltype(padded_t)::value, NEAR0 = decltype(near_t)::value;
-        const float4 wa = *reinterpret_cast<const float4 *>(wr + jb);
-        const float4 wb = *reinterpret_cast<const float4 *>(wr + jb + 4);
-        const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
-#pragma unroll
-        for (int h = 0; h < 4; h++) {
-            float2v w = {wv[2 * h], wv[2 * h + 1]};
-            if (PADDED) {  // samples past the crop are zero padding
-                const int j = jb + 2 * h;  // window index of the pair's first sample
-                w.x = j < lim ? w.x : 0.f;
-                w.y = j + 1 < lim ? w.y : 0.f;
-            }
-            canon_pair(w, canon_x2<NEAR0>(x8[2 * h], x8[2 * h + 1], cx), ea, m0, m1);
-        }
-    };
-    constexpr int R4_KV = EXTRACT_R4_KV;  // vectors per lane in one batch
-    const int rl = lane & 15, row = lane >> 4;
-    {
-        for (int gi = wid; !(DSP_ABL & 1) && 4 * gi < F; gi += NWAVE) {
-            const int g = 4 * gi + row;
-            const bool act = g < F;
-            const int gc = act ? g : F - 1;
-            const int fs = st + gc * S;
-            const int lim = min(L, en - fs);  // samples beyond the crop are zero padding
-            const bool padded = lim < L;
-            const int va = fs >> 3, vb = (fs + lim - 1) >> 3;
-            const int r = fs & 3;  // copy whose rows start at window index = -fs (mod 4)
-            const float *wr = c.wtab + r * wrow + EXTRACT_WPAD + r;  // wr[j] = w[j], j = -7 .. L + 7
-            float2v ea = {0.f, 0.f};
-            float m0 = 0.f, m1 = 0.f;
-            for (int v0 = va; v0 <= vb; v0 += 16 * R4_KV) {
-                short8 xv[R4_KV];
-#pragma unroll
-                for (int k = 0; k < R4_KV; k++) xv[k] = load_cvec(p, cur, v0 + rl + 16 * k);
-                if (vfix >= 0)  // clip-uniform, rare
-#pragma unroll
-                    for (int k = 0; k < R4_KV; k++)
-                        if (v0 + rl + 16 * k == vfix) xv[k][(n - 1) & 7] = klast;
-                auto run = [&](auto pt, auto nt) {
-#pragma unroll
-                    for (int k = 0; k < R4_KV; k++) {
-                        const int v = v0 + rl + 16 * k;
-                        if (v <= vb) frame_vec(pt, nt, xv[k], wr, 8 * v - fs, lim, ea, m0, m1);
-                    }
-                };
-                if (padded)
-                    cx.near0 ? run(BoolT<true>(), BoolT<true>()) : run(BoolT<true>(), BoolT<false>());
-                else if (cx.near0)
-                    run(BoolT<false>(), BoolT<true>());
-                else
-                    run(BoolT<false>(), BoolT<false>());
-            }
-            const float E1 = dpp_row_reduce(ea.x + ea.y, OpAdd()) * sE;
-            const float M1 = dpp_row_reduce(m0 + m1, OpAdd()) * sM;
-            // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in
-            // [j0, j1]) and j < lim; transitions into the window's zero ends / padding count too
-            const int ia = fs + j0, ib = min(fs + j1, en - 1);  // sample coords
-            int z = dpp_row_reduce(ia < ib ? chg_count(c.posw, ia + lead, ib + lead, rl, 16) : 0, OpAdd());
-            if (ia <= ib) {
-                if (j0 > 0) z += pos_bit(c.posw, ia + lead);
-                if (ib < fs + L - 1) z += pos_bit(c.posw, ib + lead);
-            }
-            if (act && rl == 0) {
-                c.fE[g] = E1;
-                c.fM[g] = M1;
-                c.fZ[g] = z;
-            }
-        }
-    }
+    // ---- R4: windowed frames over the crop [st, en) (r4_frames) --------------------------------
+    const int F = r4_frames(p, c, cur, st, en, cs, sh->j0, sh->j1, wid, lane);
     STAMP(i, 12);
     if (!FAST && F > 128)
         for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
@@ -957,49 +1089,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     const int r0 = (F - 1) / 2, r1 = F / 2;
     {
         if (FAST || F <= 128) {
-            // wave q alone handles sequence q (E, M, ZCR): lanes hold v[lane], v[lane + 64]; the
-            // order statistics by ballot ranks over readlane'd candidates, then mean / std (fp64 sums)
-            // and max / min -- no barrier
-            // six jobs (median / moments of E, M, ZCR) over the waves
-            for (int job = wid; !(DSP_ABL & 2) && job < 6; job += NWAVE) {
-                const int q = job % 3;
-                auto get = [&](int j) -> float { return q == 0 ? c.fE[j] : q == 1 ? c.fM[j] : (float)c.fZ[j]; };
-                const bool in0 = lane < F, in1 = lane + 64 < F;
-                const float x0 = in0 ? get(lane) : 0.f, x1 = in1 ? get(lane + 64) : 0.f;
-                if (job < 3) {  // median by an in-wave bitonic sort
-                    unsigned a[2] = {in0 ? fkey(x0) : ~0u, in1 ? fkey(x1) : ~0u};
-                    float v0, v1;
-                    if (F <= 64) {
-                        unsigned b[1] = {a[0]};
-                        wave_bitonic<1>(b, lane);
-                        v0 = fkey_value(sorted_at<1>(b, r0));
-                        v1 = fkey_value(sorted_at<1>(b, r1));
-                    } else {
-                        wave_bitonic<2>(a, lane);
-                        v0 = fkey_value(sorted_at<2>(a, r0));
-                        v1 = fkey_value(sorted_at<2>(a, r1));
-                    }
-                    double med;
-                    {
-#pragma clang fp contract(off)
-                        med = (F & 1) ? (double)v1 : ((double)v0 + (double)v1) / 2.0;
-                    }
-                    if (lane == 0) featb[5 * q + 4] = (float)med;
-                }
-                if (job >= 3) {  // mean, population std (fp64 sums), max, min
-                    const double s = wave_sum((in0 ? (double)x0 : 0.0) + (in1 ? (double)x1 : 0.0));
-                    const float mx = wave_reduce(fmaxf(in0 ? x0 : -INFINITY, in1 ? x1 : -INFINITY), OpMax());
-                    const float mn = wave_reduce(fminf(in0 ? x0 : INFINITY, in1 ? x1 : INFINITY), OpMin());
-                    const double mean = s / (double)F;
-                    const double d0 = in0 ? (double)x0 - mean : 0.0, d1 = in1 ? (double)x1 - mean : 0.0;
-                    const double qq = wave_sum(fma(d0, d0, d1 * d1));
-                    if (lane < 4) {
-                        const double o = lane == 0 ? mean : lane == 1 ? sqrt(qq / (double)F) : lane == 2 ? (double)mx
-                                         : (double)mn;
-                        featb[5 * q + lane] = (float)o;
-                    }
-                }
-            }
+            r5_fast(c, F, featb, wid, lane);
         } else {  // long sequences: partial ranks over all waves, then one wave per sequence
             rank_partial([&](int q, int j) { return q == 2 ? (float)c.fZ[j] : (q == 0 ? c.fE[j] : c.fM[j]); },
                          3, F, c.rank, wid, lane);
@@ -1091,7 +1181,6 @@ __device__ __forceinline__ Ctx ctx_from(const ExtractCarve &cv, unsigned char *l
     c.rank = reinterpret_cast<int *>(lds + cv.rank);
     c.pS1 = reinterpret_cast<int *>(lds + cv.pS1);
     c.pS2 = reinterpret_cast<unsigned long long *>(lds + cv.pS2);
-    c.defer = reinterpret_cast<int *>(lds + cv.defer);
     c.total = 0;
     c.stamp_clip = 0;
     return c;
@@ -1107,44 +1196,15 @@ __device__ __forceinline__ Ctx make_ctx(const ExtractParams &p, unsigned char *l
     }
 }
 
-// the rare near-tie redo, compiled out of line so its exact-order machinery does not weigh on
-// the register allocation of the streaming path.  It reads the kernel arguments where the kernel
-// received them: the kernel passes its kernarg-segment pointer (ExtractParams is the first
-// argument).  Passing the struct itself, by value or by reference, makes the kernel copy it to
-// scratch in every lane at entry (~24-60 MB of HBM writes per 1000-clip launch), and
-// __builtin_amdgcn_kernarg_segment_ptr() is null inside a called function.
-template <bool FAST>
-__device__ __attribute__((noinline)) void clip_exact(const ExtractParams *pk, int i)
+// window (create_window, :278-296) -> LDS once as four shifted zero-padded fp32 copies, and its
+// support [j0, j1] (sh->j0 / j1) by ballots: every weight read is issued before the first use, so
+// the prologue costs one L2 round trip (windows longer than WPRE * NT loop over the rest).  Ends
+// with a barrier.
+__device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &c, int tid, int lane, int wid)
 {
-    const ExtractParams &p = *pk;
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    Ctx c = make_ctx<FAST>(p, lds);
-    c.stamp_clip = i;
-    const ClipRef cr = clip_ref(p, i);
-    short8 regs[NRV];
-    issue_clip(regs, p, cr);
-    clip_body<true, FAST>(p, c, i, cr, regs);
-}
-
-// 128 VGPRs: two 512-thread workgroups per CU
-#ifndef EXTRACT_WAVES_PER_EU
-#define EXTRACT_WAVES_PER_EU 4
-#endif
-template <bool FAST>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVES_PER_EU))) void extract_kernel(ExtractParams p)
-{
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    Ctx c = make_ctx<FAST>(p, lds);
     float *wt = const_cast<float *>(c.wtab);
     Shared *sh = c.sh;
-
-    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int L = p.L, G = gridDim.x;
-    WG_STAMP(16);
-
-    // window (create_window, :278-296) -> LDS once as four shifted zero-padded fp32 copies, and
-    // its support [j0, j1] by ballots: every weight read is issued before the first use, so the
-    // prologue costs one L2 round trip (windows longer than WPRE * NT loop over the rest).
+    const int L = p.L;
     constexpr int WPRE = 3;
     double wv[WPRE];
 #pragma unroll
@@ -1152,11 +1212,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
         const int j = tid + NT * k;
         wv[k] = j < L ? p.window[j] : 0.0;
     }
-    WG_CK(18);
     if (tid == 0) {
         sh->j0 = L;
         sh->j1 = -1;
-        sh->ndefer = 0;
     }
     const int wrow = EXTRACT_WROW(L);
     for (int t = tid; t < 4 * (wrow - L); t += NT) {  // zero pads: m < WPAD + r, m >= L + WPAD + r
@@ -1164,7 +1222,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
         wt[r * wrow + (q < EXTRACT_WPAD + r ? q : q + L)] = 0.f;
     }
     __syncthreads();
-    WG_CK(19);
     auto put_weight = [&](int q0, double w) {  // weight j = q0 + lane (q0 wave-uniform)
         const int j = q0 + lane;
         const bool in = j < L;
@@ -1182,61 +1239,289 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     for (int k = 0; k < WPRE; k++) put_weight(NT * k + wid * 64, wv[k]);
     for (int q0 = NT * WPRE + wid * 64; q0 < L; q0 += NT) put_weight(q0, q0 + lane < L ? p.window[q0 + lane] : 0.0);
     __syncthreads();
-    WG_CK(20);
+}
 
-    // Clip blockIdx.x first, then clips claimed from the caller's launch-wide counter (p.queue), so
-    // that workgroups whose clips run short take more of them (a static i, i + G, ... split ends on
-    // the slowest workgroup: 3.19-3.98 ms spread at 100 000 clips); without a counter, the static
-    // split.  Thread 0 claims the next clip right after issuing the current clip's loads; the
-    // claim's latency hides behind the clip.  A workgroup claims only while its near-tie list has
-    // room for the current and the claimed clip, and the host keeps a launch at <= G *
-    // EXTRACT_DEFER_CAP / 2 clips, so the list never overflows and some workgroup can always claim
-    // what is left (statically, a workgroup gets <= EXTRACT_DEFER_CAP / 2 clips).
-    unsigned *const queue = p.queue;
-    auto next_clip = [&](int i) -> unsigned {  // thread 0 only
-        return queue ? (unsigned)G + __hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                     : (unsigned)(i + G);
-    };
+// Clips: blockIdx.x first, then clips claimed from the caller's launch-wide counter (p.queue), so
+// that workgroups whose clips run short take more of them (a static i, i + G, ... split ends on the
+// slowest workgroup: 3.19-3.98 ms spread at 100 000 clips); without a counter, the static split.
+// Thread 0 only.
+__device__ __forceinline__ unsigned claim_clip(const ExtractParams &p, unsigned &cursor)
+{
+    if (p.queue)
+        return gridDim.x + __hip_atomic_fetch_add(p.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    cursor += gridDim.x;
+    return cursor;
+}
+// the last workgroup out resets the queue for the next launch on the stream: every claim of every
+// workgroup precedes its increment of the done count.  Thread 0 only.
+__device__ __forceinline__ void queue_done(const ExtractParams &p)
+{
+    if (!p.queue) return;
+    const unsigned d = __hip_atomic_fetch_add(p.queue + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == gridDim.x - 1) {
+        __hip_atomic_store(p.queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p.queue + 1, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// 128 VGPRs: two 512-thread workgroups per CU
+#ifndef EXTRACT_WAVES_PER_EU
+#define EXTRACT_WAVES_PER_EU 4
+#endif
+
+// ---- generic layout (clips past the FAST plan): one clip at a time per workgroup -------------
+// A near tie (an endpoint decision within the certification margin) leaves the clip with status
+// DSP_CLIP_UNCERTIFIED; extract_exact_kernel, launched next on the stream, redoes it.
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVES_PER_EU))) void extract_kernel(ExtractParams p)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    Ctx c = make_ctx<false>(p, lds);
+    Shared *sh = c.sh;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    WG_STAMP(16);
+    build_window(p, c, tid, lane, wid);
     short8 regs[NRV];
     bool inflight = false;  // regs already hold clip i's loads (issued by the previous clip's R4)
+    unsigned cursor = blockIdx.x;
     for (int i = blockIdx.x; i < p.B;) {
         const ClipRef cur = clip_ref(p, i);
         unsigned claim = 0x7fffffffu;
         if (!cur.ok) {
             __syncthreads();  // everyone has read sh->next (the ok path has barriers in clip_body)
-            if (tid == 0) claim = next_clip(i);
+            if (tid == 0) claim = claim_clip(p, cursor);
             write_bad_clip(p, i, tid);
             inflight = false;
         } else {
             if (!inflight) issue_clip(regs, p, cur);
-            if (tid == 0 && (!queue || sh->ndefer < EXTRACT_DEFER_CAP - 1)) claim = next_clip(i);
+            if (tid == 0) claim = claim_clip(p, cursor);
             c.stamp_clip = i;
-            const bool done = clip_body<false, FAST>(p, c, i, cur, regs, claim);
-            if (!done && tid == 0) c.defer[sh->ndefer++] = i;
+            const bool done = clip_body<false, false>(p, c, i, cur, regs, claim);
+            if (!done && tid == 0) p.status[i] = DSP_CLIP_UNCERTIFIED;
             inflight = done;  // a deferred clip returns before R4
         }
         if (tid == 0) sh->next = (int)min(claim, 0x7fffffffu);
         __syncthreads();  // LDS summaries are rewritten by the next clip; sh->next published
         i = sh->next;
     }
-    // near ties (rare): endpoint energies in numpy's exact float64 order
-    __syncthreads();
-    const int nd = sh->ndefer;
-    for (int d = 0; d < nd; d++) {
-        const int j = c.defer[d];
-        clip_exact<FAST>((const ExtractParams *)__builtin_amdgcn_kernarg_segment_ptr(), j);
+    if (tid == 0) queue_done(p);
+    WG_STAMP(22);
+}
+
+// ---- FAST layout: two clips in flight per workgroup ------------------------------------------
+// Word r of thread tid: waves 1 .. NWAVE-1 hold the first (NT - 64) RREG words of the clip, wave 0
+// -- which runs the previous clip's endpoint scan while the others run R1 -- the rest (35 words of
+// a 1 s clip).
+__device__ __forceinline__ int pipe_word(int r, int tid)
+{
+    return tid >= 64 ? r * (NT - 64) + (tid - 64) : (NT - 64) * RREG + 64 * r + tid;
+}
+__device__ __forceinline__ void issue_clip_pipe(short8 (&regs)[NRV], const ExtractParams &p, const ClipRef &c, int tid)
+{
+#pragma unroll
+    for (int r = 0; r < RREG; r++) issue_word(&regs[4 * r], p, c, pipe_word(r, tid));
+}
+
+// The persistent loop keeps two clips in flight: B (the newer, whose words arrive in registers)
+// and A (the older, whose summaries are in LDS).  Each trip runs four barrier-separated stages:
+//   S1  wave 0: A's double-threshold scan;  waves 1-7 (+ wave 0 after it): B's R1 from registers
+//   S2  B's mean / peak, R2 (positive bits) and its pass-A partial-word loads; A's crop [st, en)
+//   S3  B's VAD frames (energies, ZCR);  A's windowed crop frames (R4)
+//   S4  the next clip's loads;  waves 0-5: A's 15 statistics (R5);  wave 6: B's p90;  wave 7: B's
+//       noise estimates
+// so the single-wave phases of one clip (scan, p90) run beside the multi-wave phases of the
+// other.  Per clip slot (A and B alternate between slots 0 and 1): the Shared record and the
+// positive bits; the word moments, VAD arrays and frame arrays are single (each is dead by the
+// time the other clip writes it).  A near tie leaves the clip DSP_CLIP_UNCERTIFIED for
+// extract_exact_kernel.
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVES_PER_EU))) void extract_pipe_kernel(ExtractParams p)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    constexpr ExtractCarve cv = extract_carve_fast();
+    const Ctx c0 = ctx_from(cv, lds);
+    Shared *const shs0 = c0.sh;
+    Shared *const shs1 = reinterpret_cast<Shared *>(lds + cv.sh2);
+    uint32_t *const posw0 = c0.posw;
+    uint32_t *const posw1 = reinterpret_cast<uint32_t *>(lds + cv.posw2);
+    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int L = p.L, S = p.S;
+    WG_STAMP(16);
+    build_window(p, c0, (int)threadIdx.x, (int)threadIdx.x & 63, wid);
+    const int j0 = uni(shs0->j0), j1 = uni(shs0->j1);
+
+    unsigned cursor = blockIdx.x;
+    int inext = (int)blockIdx.x < p.B ? (int)blockIdx.x : -1;  // the clip whose words are in flight
+    ClipRef rnext = inext >= 0 ? clip_ref(p, inext) : clip_none();
+    short8 regs[NRV];
+    issue_clip_pipe(regs, p, rnext, (int)threadIdx.x);
+
+    int ia = -1, ib = -1, slotB = 1;
+    bool okA = false, okB = false;
+    ClipRef ra = clip_none(), rb = clip_none();
+    ClipStats sa{}, sb{};
+    for (;;) {
+        // rotate: B -> A, the in-flight clip -> B
+        ia = ib;
+        ra = rb;
+        sa = sb;
+        okA = okB;
+        ib = inext;
+        rb = rnext;
+        okB = ib >= 0 && rb.ok;
+        slotB ^= 1;
+        if (ia < 0 && ib < 0) break;
+        // the thread index, opaque to the optimiser once per trip: index arithmetic that depends
+        // only on it (word numbers, lane masks of the sorts) is then recomputed in the trip instead
+        // of being hoisted out of the loop and kept live (spilled) across it
+        int tid = (int)threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int lane = tid & 63;
+        Shared *const shA = slotB ? shs0 : shs1, *const shB = slotB ? shs1 : shs0;
+        Ctx cA = c0, cB = c0;
+        cA.sh = shA;
+        cA.posw = slotB ? posw0 : posw1;
+        cB.sh = shB;
+        cB.posw = slotB ? posw1 : posw0;
+        STAMP(ib >= 0 ? ib : 0, 0);
+
+        // ---- S1 --------------------------------------------------------------------------------
+        if (tid == 0) {
+            int nx = -1;
+            if (ib >= 0) {
+                const unsigned cl = claim_clip(p, cursor);
+                nx = cl < (unsigned)p.B ? (int)cl : -1;
+            }
+            shs0->next = nx;
+        }
+        if (wid == 0 && okA && sa.nv > 0) {
+            // the scan is the trip's single-wave critical path: issue priority over the
+            // co-resident workgroup's waves
+            __builtin_amdgcn_s_setprio(2);
+            const int flag = vad_scan<true, true>(p, cA, sa.nv, lane);
+            if (lane == 0) shA->exact = sa.Mp > 0.0 ? flag : 0;
+            __builtin_amdgcn_s_setprio(0);
+        }
+        if (okB) {
+            R1Acc acc = r1_acc_init();
+            const int nword = rb.nword;
+#pragma unroll
+            for (int r = 0; r < RREG; r++) {
+                const int w = pipe_word(r, tid);
+                if (w < nword) r1_word(&regs[4 * r], w, nword, rb.lead, rb.n, acc, c0.wS1, c0.wS2);
+            }
+            r1_reduce(acc, shB, wid, lane);
+        }
+        STAMP(ib >= 0 ? ib : 0, 1);
+        __syncthreads();  // B1
+
+        // ---- S2 --------------------------------------------------------------------------------
+        if (okB) sb = clip_stats(shB, rb.n, L, S, p.do_vad);
+        int st = 0, en = ra.n;
+        bool actA = okA;
+        if (okA && sa.nv > 0) {
+            if (uni(shA->exact)) {  // near tie: redone in numpy's exact order by extract_exact_kernel
+                actA = false;
+                if (tid == 0) p.status[ia] = DSP_CLIP_UNCERTIFIED;
+            } else {
+                if (uni(shA->n3) >= 0) {
+                    st = uni(shA->n1) * S;              // :272
+                    en = min(uni(shA->n6) * S + L, ra.n);  // :273
+                }
+                if (p.vad_energy)  // before S3 rewrites the VAD arrays
+                    for (int f = tid; f < sa.nv && f < p.ld_vad; f += NT) {
+                        p.vad_energy[(size_t)ia * p.ld_vad + f] = c0.vE[f];
+                        p.vad_zcr[(size_t)ia * p.ld_vad + f] = c0.vZ[f];
+                    }
+            }
+        }
+        if (ib >= 0 && !okB) write_bad_clip(p, ib, tid);  // empty or longer than the launch's cap
+        short8 qa[4];
+        int pa_w = -1, pa_e0 = 0, pa_e1 = 0;
+        if (okB) {
+            const int nword = rb.nword;
+#pragma unroll
+            for (int r = 0; r < RREG; r++) {
+                const int w = pipe_word(r, tid);
+                if (w < nword)
+                    cB.posw[w] = (DSP_ABL & 4) ? 0u : pos_word(&regs[4 * r], w, nword, rb.lead, rb.n, sb.tpos);
+            }
+            if (tid < 2) cB.posw[nword + tid] = 0;
+            // the partial words of pass A, in flight across the barrier
+            if (sb.nv > 0) pa_w = vad_partial_issue(p, rb, L, S, sb.nv, tid, qa, pa_e0, pa_e1);
+        }
+        inext = uni(shs0->next);
+        rnext = inext >= 0 ? clip_ref(p, inext) : clip_none();
+        STAMP(ib >= 0 ? ib : 0, 2);
+        __syncthreads();  // B2
+
+        // ---- S3 --------------------------------------------------------------------------------
+        if (okB && sb.nv > 0) vad_frames_fast(cB, rb, L, S, sb, qa, pa_w, pa_e0, pa_e1, tid);
+        STAMP(ib >= 0 ? ib : 0, 7);
+        int F = 0;
+        if (actA) F = r4_frames(p, cA, ra, st, en, sa, j0, j1, NWAVE - 1 - wid, lane);  // waves 7, 6, .. first
+        STAMP(ia >= 0 ? ia : 0, 12);
+        __syncthreads();  // B3
+
+        // ---- S4 --------------------------------------------------------------------------------
+        // regs are dead since R2: the next clip's words load during S4 and S1 (unconditional, a
+        // clip_none() reads zeros, so the compiler's vmcnt bookkeeping stays exact)
+        issue_clip_pipe(regs, p, rnext, tid);
+        if (actA) {
+            r5_fast(c0, F, p.feat + (size_t)ia * 15, wid, lane);
+            if (p.seq)
+                for (int g = tid; g < F && g < p.ld_seq; g += NT) {
+                    float *o = p.seq + ((size_t)ia * p.ld_seq + g) * 3;
+                    o[0] = c0.fE[g];
+                    o[1] = c0.fM[g];
+                    o[2] = (float)c0.fZ[g];
+                }
+            if (tid == 0) {
+                p.start_end[2 * ia] = st;
+                p.start_end[2 * ia + 1] = en;
+                p.n_frames[ia] = F;
+                p.status[ia] = DSP_CLIP_OK;
+            }
+        }
+        STAMP(ia >= 0 ? ia : 0, 9);
+        if (okB && sb.nv > 0) {
+            if (wid == NWAVE - 2) {  // p90 order statistics (:198), then the scan: critical path
+                __builtin_amdgcn_s_setprio(2);
+                p90_select_wave(cB, sb.nv, lane);
+                __builtin_amdgcn_s_setprio(0);
+            } else if (wid == NWAVE - 1) {
+                vad_noise(cB, sb.nv, lane);
+            }
+        }
+        STAMP(ib >= 0 ? ib : 0, 3);
+        __syncthreads();  // B4
+    }
+    if (threadIdx.x == 0) queue_done(p);
+    WG_STAMP(22);
+}
+
+// ---- near ties: the endpoint energies in numpy's exact float64 order ----------------------------
+// Launched after extract_pipe_kernel / extract_kernel on the same stream: every clip they left
+// DSP_CLIP_UNCERTIFIED (rare) is redone from the start by one workgroup, on the bit-exact
+// (numpy-order) energy path, and gets its final outputs and DSP_CLIP_FLAG_VAD_EXACT.
+template <bool FAST>
+__global__ __launch_bounds__(NT) void extract_exact_kernel(ExtractParams p)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    Ctx c = make_ctx<FAST>(p, lds);
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    bool built = false;
+    for (int i = blockIdx.x; i < p.B; i += gridDim.x) {
+        if (__builtin_amdgcn_readfirstlane(p.status[i]) != DSP_CLIP_UNCERTIFIED) continue;
+        if (!built) {
+            build_window(p, c, tid, lane, wid);
+            built = true;
+        }
+        c.stamp_clip = i;
+        const ClipRef cr = clip_ref(p, i);
+        short8 regs[NRV];
+        issue_clip(regs, p, cr);
+        clip_body<true, FAST>(p, c, i, cr, regs);
         __syncthreads();
     }
-    // the last workgroup out resets the queue for the next launch on the stream: every claim of
-    // every workgroup precedes its increment of the done count
-    if (tid == 0 && queue) {
-        const unsigned d = __hip_atomic_fetch_add(queue + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (d == (unsigned)G - 1) {
-            __hip_atomic_store(queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(queue + 1, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    WG_STAMP(22);
 }
 
 }  // namespace dsp
@@ -1254,13 +1539,12 @@ extern "C" size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int f
 {
     if (max_len < 1 || frame_length < 1 || frame_shift < 1) return 0;
     if (max_len > (1 << 24) || frame_length > (1 << 20)) return 0;
-    const ExtractCarve c = extract_carve((int)max_len, frame_length, frame_shift, EXTRACT_DEFER_CAP);
+    const ExtractCarve c = extract_carve((int)max_len, frame_length, frame_shift);
     return c.total <= EXTRACT_LDS_LIMIT ? (size_t)c.total : 0;
 }
 
 // CU count per device (the persistent grid), cached on first use of each device
 static int g_num_cus[64];
-static_assert(EXTRACT_DEFER_CAP >= 2, "the claim rule keeps room for two clips");
 
 extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, int B,
                                     int64_t max_len, int frame_length, int frame_shift,
@@ -1285,9 +1569,13 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return DSP_ERR_HIP;
         g_num_cus[dev] = prop.multiProcessorCount;
-        (void)hipFuncSetAttribute((const void *)dsp::extract_kernel<true>,
+        (void)hipFuncSetAttribute((const void *)dsp::extract_pipe_kernel,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
-        (void)hipFuncSetAttribute((const void *)dsp::extract_kernel<false>,
+        (void)hipFuncSetAttribute((const void *)dsp::extract_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
+        (void)hipFuncSetAttribute((const void *)dsp::extract_exact_kernel<true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
+        (void)hipFuncSetAttribute((const void *)dsp::extract_exact_kernel<false>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
     }
     const int num_cus = g_num_cus[dev];
@@ -1314,41 +1602,23 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     p.ld_seq = ld_seq;
     p.stamps = (unsigned long long *)g_stamp_buffer;
     p.queue = (unsigned *)queue_ws;
-    p.cv = extract_carve((int)max_len, frame_length, frame_shift, EXTRACT_DEFER_CAP);
+    p.cv = extract_carve((int)max_len, frame_length, frame_shift);
     // persistent grid: two workgroups per CU when their LDS fits (one otherwise), each walking
-    // clip blockIdx first, then clips from the launch's queue; the compile-time layout whenever
-    // the launch fits it
+    // clip blockIdx first, then clips from the launch's queue; the compile-time layout (and the
+    // two-clip pipeline) whenever the launch fits it
     const bool fast = extract_fast_fits((int)max_len, frame_length, frame_shift);
     const size_t lds_launch = fast ? (size_t)extract_carve_fast().total : lds;
     const int per_cu = std::max(1, std::min<int>(EXTRACT_WG_PER_CU, (int)(EXTRACT_LDS_LIMIT / lds_launch)));
     const int slots = per_cu * num_cus;
-    // at most EXTRACT_DEFER_CAP / 2 clips per workgroup and launch on average (see the claim rule
-    // in extract_kernel), so every near tie fits its workgroup's redo list (larger batches:
-    // consecutive launches on the stream)
-    const int64_t chunk = (int64_t)slots * (EXTRACT_DEFER_CAP / 2);
-    for (int64_t b0 = 0; b0 < B; b0 += chunk) {
-        dsp::ExtractParams q = p;
-        const int nb = (int)std::min<int64_t>(chunk, B - b0);
-        q.B = nb;
-        q.offsets = offsets + b0;
-        q.feat = feat + 15 * b0;
-        q.start_end = start_end + 2 * b0;
-        q.n_frames = n_frames + b0;
-        q.status = status + b0;
-        if (vad_energy) {
-            q.vad_energy = vad_energy + b0 * ld_vad;
-            q.vad_zcr = vad_zcr + b0 * ld_vad;
-        }
-        if (seq) q.seq = seq + b0 * ld_seq * 3;
-        if (q.stamps) q.stamps = p.stamps + 32 * b0;
-        const int grid = nb < slots ? nb : slots;
-        if (fast)
-            hipLaunchKernelGGL(dsp::extract_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch, (hipStream_t)stream, q);
-        else
-            hipLaunchKernelGGL(dsp::extract_kernel<false>, dim3(grid), dim3(dsp::NT), lds_launch, (hipStream_t)stream, q);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return DSP_ERR_HIP + (int)e;
+    const int grid = B < slots ? B : slots;
+    const hipStream_t s = (hipStream_t)stream;
+    if (fast) {
+        hipLaunchKernelGGL(dsp::extract_pipe_kernel, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
+        hipLaunchKernelGGL(dsp::extract_exact_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
+    } else {
+        hipLaunchKernelGGL(dsp::extract_kernel, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
+        hipLaunchKernelGGL(dsp::extract_exact_kernel<false>, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
     }
-    return DSP_OK;
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? DSP_OK : DSP_ERR_HIP + (int)e;
 }
-

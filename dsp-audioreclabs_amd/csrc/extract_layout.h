@@ -18,9 +18,6 @@
 #define EXTRACT_WG_PER_CU 2              // resident workgroups per CU the register budget allows
 #endif
 #define EXTRACT_LDS_LIMIT (160 * 1024)   // one CU
-#ifndef EXTRACT_DEFER_CAP
-#define EXTRACT_DEFER_CAP 512            // near-tie clips one workgroup can redo exactly
-#endif
 #define EXTRACT_SHARED_BYTES 512         // sizeof(dsp::Shared) rounded up (static_assert'ed)
 #define EXTRACT_WPAD 8                   // zero window entries on each side of the window table
 // floats per shifted window copy: copy r holds w[m - WPAD - r] at m (zero outside [0, L)), so
@@ -28,14 +25,15 @@
 #define EXTRACT_WROW(L) ((((L) + 2 * EXTRACT_WPAD + 4) + 3) & ~3)
 
 struct ExtractCarve {
-    int sh, wtab, posw, wS2, wS1, vE, vZ, fE, fM, fZ, rank, pS2, pS1, defer, total;
+    int sh, wtab, posw, wS2, wS1, vE, vZ, fE, fM, fZ, rank, pS2, pS1, sh2, posw2, total;
     int nvcap, fcap, nwmax;
 };
 
 // Region offsets from the capacities: nwmax 32-sample words (incl. the alignment lead), nvcap VAD
-// frames, fcap feature frames, wrow floats per shifted window copy, per_wg deferred clips.
-__host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvcap, int fcap, int wrow, int per_wg,
-                                                              bool rank = true)
+// frames, fcap feature frames, wrow floats per shifted window copy.  pipe: the second clip slot of
+// the pipelined FAST kernel (its Shared record and positive bits).
+__host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvcap, int fcap, int wrow,
+                                                              bool rank = true, bool pipe = false)
 {
     ExtractCarve c{};
     int o = 0;
@@ -60,19 +58,20 @@ __host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvc
     DSP_TAKE(rank, rank ? 4 * (c.nvcap > 3 * c.fcap ? c.nvcap : 3 * c.fcap) : 0);  // long clips only
     DSP_TAKE(pS2, 16 * c.nvcap);  // partial-word moments at the two ends of each VAD frame
     DSP_TAKE(pS1, 8 * c.nvcap);
-    DSP_TAKE(defer, 4 * per_wg);
+    DSP_TAKE(sh2, pipe ? EXTRACT_SHARED_BYTES : 0);
+    DSP_TAKE(posw2, pipe ? 4 * (c.nwmax + 2) : 0);
 #undef DSP_TAKE
     c.total = o;
     return c;
 }
 
 // ncap = longest clip of the launch (samples)
-__host__ __device__ inline ExtractCarve extract_carve(int ncap, int L, int S, int per_wg)
+__host__ __device__ inline ExtractCarve extract_carve(int ncap, int L, int S)
 {
     const int nvcap = ncap >= L ? (ncap - L) / S + 1 : 0;
     const int fcap = ncap <= L ? 1 : (ncap - L + S - 1) / S + 1;
     const int nwmax = (ncap + 7 + 31) / 32 + 1;
-    return extract_carve_caps(nwmax, nvcap, fcap, EXTRACT_WROW(L), per_wg);
+    return extract_carve_caps(nwmax, nvcap, fcap, EXTRACT_WROW(L));
 }
 
 // The fast kernel's layout is fixed at compile time (every LDS address an immediate) and serves
@@ -86,12 +85,12 @@ __host__ __device__ inline ExtractCarve extract_carve(int ncap, int L, int S, in
 #define EXTRACT_FAST_NWORD (EXTRACT_THREADS * EXTRACT_RREG)
 __host__ __device__ constexpr ExtractCarve extract_carve_fast()
 {
-    return extract_carve_caps(EXTRACT_FAST_NWORD + 1, EXTRACT_FAST_NV, EXTRACT_FAST_NF, EXTRACT_FAST_WROW,
-                              EXTRACT_DEFER_CAP, false);
+    return extract_carve_caps(EXTRACT_FAST_NWORD + 1, EXTRACT_FAST_NV, EXTRACT_FAST_NF, EXTRACT_FAST_WROW, false,
+                              true);
 }
 __host__ __device__ inline bool extract_fast_fits(int ncap, int L, int S)
 {
-    const ExtractCarve c = extract_carve(ncap, L, S, EXTRACT_DEFER_CAP);
+    const ExtractCarve c = extract_carve(ncap, L, S);
     return (ncap + 7 + 31) / 32 <= EXTRACT_FAST_NWORD && c.nvcap <= EXTRACT_FAST_NV &&
            c.fcap <= EXTRACT_FAST_NF && EXTRACT_WROW(L) <= EXTRACT_FAST_WROW;
 }

@@ -46,12 +46,11 @@ extern "C" {
 #define DSP_CLIP_NO_FRAMES 3  /* "No frames provided ..." (feature_extraction.py:27-28) */
 #define DSP_CLIP_TOO_LONG 4   /* longer than the max_len given at launch (dsp_extract_general
                                  processes such clips) */
-#define DSP_CLIP_UNCERTIFIED 5 /* reserved: an endpoint decision that could not be certified.
-                                  Never produced: a workgroup claims clips only while its
-                                  near-tie list has room (statically it gets at most half the
-                                  list's capacity) and launches hold at most
-                                  G x EXTRACT_DEFER_CAP / 2 clips, so every near tie is redone
-                                  on the exact path */
+#define DSP_CLIP_UNCERTIFIED 5 /* internal, never left in status on return of the stream:
+                                  the fused kernel marks a clip whose endpoint decision is a
+                                  near tie (within the 1e-11 certification margin) with it, and
+                                  the exact kernel that dsp_extract_features launches next on
+                                  the same stream redoes every such clip on the bit-exact path */
 /* status[b] flag bits (informational) */
 #define DSP_CLIP_FLAG_VAD_EXACT 0x100 /* endpoint decision was a near tie: re-decided on the
                                          bit-exact (numpy-order) fp64 path */
@@ -61,7 +60,9 @@ extern "C" {
 size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int frame_shift);
 
 /*
- * dsp_extract_features -- fused per-clip pipeline, one workgroup per clip.
+ * dsp_extract_features -- fused per-clip pipeline: persistent workgroups (two per CU), each
+ * keeping two clips in flight (one in registers, one in LDS summaries), then a second launch on
+ * the same stream that redoes near-tie endpoint decisions on the bit-exact path.
  * Replaces, per clip, the chain
  *   preprocess            src/audio_processing.py:78-90   (remove_dc :49-59, normalize_audio :62-75)
  *   endpoint_detection    src/audio_processing.py:135-275 (when do_vad != 0)

@@ -101,9 +101,9 @@ def test_production_12500_per_rank_batch(win):
     _check(out, clips, create_window(win, L), idx=range(0, B, 12))
 
 
-def test_chunked_launch_over_defer_cap():
-    """More clips than one launch may hold (G x EXTRACT_DEFER_CAP / 2 = 131 072 on MI355X): the
-    host splits the batch into consecutive launches; clips on both sides of each split match."""
+def test_large_batch_one_launch():
+    """More clips than the persistent grid's slots x 256 (the round-3 launch-chunking boundary, now
+    one launch): clips on both sides of the old boundary and at the end match the oracle."""
     import torch
     from src.pipeline import FeatureExtractor, create_window
     from src.synth import make_batch_device
@@ -170,15 +170,12 @@ def test_sharded_knn_self_query_equals_single():
     assert np.array_equal(p_full.cpu().numpy()[lo:hi], p0)
 
 
-def test_small_defer_cap_variant():
-    """The clip queue's claim rule under pressure.  lib/libdsp_audiorec_cap4.so (Makefile) is the
-    product kernel built with a near-tie list of 4 clips per workgroup: a workgroup stops claiming
-    once 3 near ties are listed, and a launch holds G x 4 / 2 clips.  Every third clip of a
-    5G + 37-clip batch is a near tie (3 launches, the last ragged); every clip must be processed,
-    match the oracle, and the near ties must have been redone exactly."""
-    import os
+def test_many_near_ties():
+    """Near ties under pressure: every third clip of a 5G + 37-clip batch is a near tie, so both
+    slots of the fused kernel's two-clip pipeline hit them back to back.  Each is left
+    DSP_CLIP_UNCERTIFIED by extract_pipe_kernel and redone by extract_exact_kernel on the same
+    stream: every clip must match the oracle and every near tie carry DSP_CLIP_FLAG_VAD_EXACT."""
     import torch
-    from src import _hip
     from src.pipeline import FeatureExtractor, create_window
     from src.synth import make_batch
     G = 2 * torch.cuda.get_device_properties(0).multi_processor_count
@@ -189,14 +186,8 @@ def test_small_defer_cap_variant():
     off = np.zeros(B + 1, np.int64)
     off[1:] = np.cumsum([c.size for c in clips])
     pcm = torch.as_tensor(np.concatenate(clips + [np.zeros(8, np.int16)])).cuda()
-    path = os.path.join(os.path.dirname(_hip.LIB_PATH), "libdsp_audiorec_cap4.so")
-    saved = _hip._lib
-    _hip._lib = None
-    try:
-        _hip.load_library(path)
-        fx = FeatureExtractor(L, S, "hamming", True)
-        out = {k: v.cpu().numpy() for k, v in fx(pcm, off).items()}
-    finally:
-        _hip._lib = saved
+    fx = FeatureExtractor(L, S, "hamming", True)
+    out = {k: v.cpu().numpy() for k, v in fx(pcm, off).items()}
     _check(out, clips, create_window("hamming", L))
     assert ((out["status"][::3] >> 8) & 1).all(), "near ties were not redone exactly"
+    assert not ((out["status"][1::3] >> 8) & 1).any()

@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 400 python3 $R/bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err
 cat $OUT/bench.json
-H="--no-cpu --sweep-clips 0 --knn-ref 0"
+H="--no-cpu --sweep-clips 0 --knn-ref 0 --no-cfg0 --small-clips 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 $R/bench.py $H "$@" > $OUT/kt.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc -- python3 $R/bench.py $H --steps 8 --warmup 1 "$@" > $OUT/pmc_fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pmc -- python3 $R/bench.py $H --steps 8 --warmup 1 "$@" > $OUT/pmc_write.log 2>&1
