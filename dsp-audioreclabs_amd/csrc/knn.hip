@@ -205,11 +205,22 @@ static constexpr int MQ_TR = KNN_MQ_TR;                // reference rows per LDS
 __host__ __device__ constexpr int mq_stride(int DP) { return DP + 4; }  // conflict-free 16-B reads
 typedef float mq_f4 __attribute__((ext_vector_type(4)));
 // lane_xor_f (dsp_device.h): the value of lane ^ 16 / lane ^ 32 by the gfx950 permlane swaps
+//
+// Seeded thresholds: with `seed` non-null each query's threshold starts at seed[q] instead of +inf
+// (knn_seed: the KC-th smallest distance over a strided sample of the reference rows, which bounds
+// the KC-th smallest of the whole set from above), so a split no longer pays the list warm-up of a
+// threshold at +inf -- nearly every 16-row step inserting while the lists fill.  A row is kept only
+// below min(seed, the lists' thresholds); knn_merge starts its screening cut-off at the seed, so a
+// query whose seed was too tight fails certification and is answered by the exhaustive fallback:
+// exactness never depends on the seed.
+// The same kernel screens that sample (the pilot): rows are the sample's, sample row j = reference
+// row j * rstride (rstride = 1: every row), and the query's own row is masked in global numbering.
 template <int DP, int KC>
 __global__ __launch_bounds__(64 * MQ_W) void knn_screen_mfma(const float *__restrict__ ref32, int64_t Nr,
                                                            const float *__restrict__ q32, int64_t Nq,
                                                            int64_t self_offset, int nsplit,
-                                                           float *__restrict__ cand_d, int *__restrict__ cand_i)
+                                                           float *__restrict__ cand_d, int *__restrict__ cand_i,
+                                                           int rstride, const float *__restrict__ seed)
 {
     constexpr int RS = mq_stride(DP), NJ = DP / 4, NV = DP / 16;
     constexpr int MQ_T = mq_tiles(KC), MQ_QPB = mq_qpb(KC);
@@ -217,11 +228,13 @@ __global__ __launch_bounds__(64 * MQ_W) void knn_screen_mfma(const float *__rest
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int col = lane & 15, rg = lane >> 4;
     const int sp = blockIdx.y;
-    const int64_t per = (Nr + nsplit - 1) / nsplit;
+    const int64_t per = (Nr + nsplit - 1) / nsplit;  // Nr: rows of the (sampled) set
     const int64_t r0 = (int64_t)sp * per, r1 = min(Nr, r0 + per);
     const int64_t wq0 = (int64_t)blockIdx.x * MQ_QPB + wid * MQ_T * 16;  // the wave's first query
-    // rows that can be one of the wave's own queries (self_offset >= 0): [slo, slo + 16 MQ_T)
-    const int64_t slo = self_offset >= 0 ? self_offset + wq0 : INT64_MIN / 2;
+    // sample rows that can be one of the wave's own queries (self_offset >= 0): [slo, shi)
+    const int64_t g0 = self_offset + wq0, g1 = g0 + 16 * MQ_T;
+    const int64_t slo = self_offset >= 0 ? (g0 + rstride - 1) / rstride : INT64_MIN / 2;
+    const int64_t shi = self_offset >= 0 ? (g1 + rstride - 1) / rstride : INT64_MIN / 2;
     int64_t q[MQ_T], self[MQ_T];
     float qb[MQ_T][NJ], qn[MQ_T], tau[MQ_T];
     float dl[MQ_T][KC];
@@ -242,8 +255,10 @@ __global__ __launch_bounds__(64 * MQ_W) void knn_screen_mfma(const float *__rest
             qb[t][4 * h + 2] = v.z;
             qb[t][4 * h + 3] = v.w;
         }
-        self[t] = (self_offset >= 0 && q[t] < Nq) ? self_offset + q[t] : -1;
-        tau[t] = INFINITY;
+        // the query's own row as a sample row (-1: not in the sample)
+        const int64_t sg = (self_offset >= 0 && q[t] < Nq) ? self_offset + q[t] : -1;
+        self[t] = (sg >= 0 && sg % rstride == 0) ? sg / rstride : -1;
+        tau[t] = (seed && q[t] < Nq) ? seed[q[t]] : INFINITY;
 #pragma unroll
         for (int i = 0; i < KC; i++) {
             dl[t][i] = INFINITY;
@@ -257,7 +272,7 @@ __global__ __launch_bounds__(64 * MQ_W) void knn_screen_mfma(const float *__rest
             const int row = e / (DP / 4), c4 = e % (DP / 4);
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
             if (row < nt)
-                v = reinterpret_cast<const float4 *>(ref32 + (t0 + row) * DP)[c4];
+                v = reinterpret_cast<const float4 *>(ref32 + (t0 + row) * rstride * DP)[c4];
             else if (c4 == DP / 4 - 1)
                 v.w = INFINITY;  // |r|^2 of a padding row: distance +inf
             *reinterpret_cast<float4 *>(tile + row * RS + 4 * c4) = v;
@@ -282,7 +297,7 @@ __global__ __launch_bounds__(64 * MQ_W) void knn_screen_mfma(const float *__rest
 #pragma unroll
                 for (int t = 0; t < MQ_T; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], qb[t][j], acc[t], 0, 0, 0);
             const int64_t rb = t0 + s0;  // the step's first row
-            if (rb < slo + 16 * MQ_T && rb + 16 > slo)  // wave-uniform: a query's own row may be here
+            if (rb < shi && rb + 16 > slo)  // wave-uniform: a query's own row may be here
                 for (int t = 0; t < MQ_T; t++)
                     for (int v = 0; v < 4; v++)
                         if (rb + 4 * rg + v == self[t]) acc[t][v] = INFINITY;
@@ -297,7 +312,7 @@ __global__ __launch_bounds__(64 * MQ_W) void knn_screen_mfma(const float *__rest
                     float th = dl[t][KC - 1];
                     th = fminf(th, lane_xor_f(th, 16, lane));
                     th = fminf(th, lane_xor_f(th, 32, lane));
-                    tau[t] = th;
+                    tau[t] = fminf(tau[t], th);  // = min(seed, the lists' thresholds)
                 }
             }
         }
@@ -325,10 +340,37 @@ __global__ __launch_bounds__(64 * MQ_W) void knn_screen_mfma(const float *__rest
 #pragma unroll
             for (int i = 0; i < KC; i++) {
                 cand_d[o + i] = dl[t][i];
-                cand_i[o + i] = il[t][i];
+                if (cand_i) cand_i[o + i] = il[t][i];
             }
         }
     }
+}
+
+// the seed of each query: the KC-th smallest of the pilot's nsplit x KC screened distances (the KC
+// smallest of the sample), one thread per query
+template <int KC>
+__global__ __launch_bounds__(256) void knn_seed(const float *__restrict__ cand_d, int nsplit, int64_t Nq,
+                                                float *__restrict__ seed, float scale)
+{
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= Nq) return;
+    float k32[KC];
+#pragma unroll
+    for (int i = 0; i < KC; i++) k32[i] = INFINITY;
+    for (int s = 0; s < nsplit; s++) {
+        const float *c = cand_d + ((size_t)s * Nq + q) * KC;
+#pragma unroll
+        for (int i = 0; i < KC; i++) {
+            float v = c[i];
+#pragma unroll
+            for (int j = 0; j < KC; j++) {
+                const float lo = fminf(v, k32[j]);
+                v = fmaxf(v, k32[j]);
+                k32[j] = lo;
+            }
+        }
+    }
+    seed[q] = k32[KC - 1] * scale;  // scale: 1 (< 1 only in the diagnostic build's tests)
 }
 
 // High-dimensional rows (D > 32: the sequence method's flattened (E, ZCR) sequences,
@@ -505,7 +547,7 @@ __global__ __launch_bounds__(64) void knn_merge(const double *__restrict__ ref, 
                           const unsigned int *maxnorm_bits, double err_rel, double err_abs,
                           const int32_t *__restrict__ labels, int32_t *__restrict__ idx,
                           double *__restrict__ dist, int32_t *__restrict__ pred, int *fb_count,
-                          int *fb_list)
+                          int *fb_list, const float *__restrict__ seed)
 {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= Nq) return;
@@ -529,7 +571,9 @@ __global__ __launch_bounds__(64) void knn_merge(const double *__restrict__ ref, 
     float k32[KM];
 #pragma unroll
     for (int i = 0; i < KM; i++) k32[i] = INFINITY;
-    float kth = INFINITY, cut = INFINITY;
+    // cut: every row the screen did not keep has a screened distance >= cut (a seeded screen keeps
+    // only rows below min(seed, the lists' thresholds))
+    float kth = INFINITY, cut = seed ? seed[q] : INFINITY;
     for (int s = 0; s < nsplit; s++) {
         const size_t o = ((size_t)s * Nq + q) * KC;
         int rr[KC];
@@ -702,14 +746,26 @@ __global__ void zscore_apply_kernel(const double *X, int64_t N, int D, const dou
 // ------------------------------------------------------------------------------------------
 namespace {
 struct KnnLayout {
-    size_t ref32, q32, cand_d, cand_i, misc, total;
+    size_t ref32, q32, cand_d, cand_i, misc, pilot_d, seed, total;
     int DP, KC, nsplit;
+    int rstride, nsample, nsplit_p;  // seeded thresholds (rstride > 0): sample rows j * rstride
     bool exp;  // expanded-form screening (a spare padded column holds |r|^2)
     bool hd;   // D > 32: chunked direct-form screen (knn_screen_hd)
     bool mfma; // expanded form on the matrix cores (knn_screen_mfma)
 };
 
 static constexpr int KNN_DMAX = 4096;
+// seeded thresholds: a pilot over ~KNN_SEED_SAMPLE strided rows when the set has >= KNN_SEED_MIN_NR;
+// the split model's warm-up term after seeding (rows)
+#ifndef KNN_SEED_SAMPLE
+#define KNN_SEED_SAMPLE 4096
+#endif
+#ifndef KNN_SEED_MIN_NR
+#define KNN_SEED_MIN_NR 32768
+#endif
+#ifndef KNN_SEED_WARM
+#define KNN_SEED_WARM 3072.0
+#endif
 
 int pick_kc(int k)
 {
@@ -721,9 +777,10 @@ int pick_kc(int k)
 }
 
 // MFMA screen: reference splits.  Every workgroup of the grid is resident at once, so a CU's time
-// is (rows per split + a split's list warm-up, ~16k rows) x its waves, and a CU saturates at
-// about two waves per SIMD:  T(s) = (Nr / s + 16k) * max(waves on the busiest CU, 8).
-int pick_nsplit_mfma(int64_t Nr, int64_t Nq, int qpb, int cus)
+// is (rows per split + a split's list warm-up W) x its waves, and a CU saturates at about two
+// waves per SIMD:  T(s) = (Nr / s + W) * max(waves on the busiest CU, 8).  W ~ 16k rows from a
+// threshold at +inf; far less from a seeded threshold.
+int pick_nsplit_mfma(int64_t Nr, int64_t Nq, int qpb, int cus, double warm = 16384.0)
 {
     const int64_t qblocks = (Nq + qpb - 1) / qpb;
     const int64_t maxs = std::max<int64_t>(1, std::min<int64_t>(64, (Nr + dsp::MQ_TR - 1) / dsp::MQ_TR));
@@ -731,7 +788,7 @@ int pick_nsplit_mfma(int64_t Nr, int64_t Nq, int qpb, int cus)
     double best_t = 1e300;
     for (int64_t s = 1; s <= maxs; s++) {
         const int64_t waves = (qblocks * s + cus - 1) / cus * dsp::MQ_W;
-        const double t = ((double)Nr / (double)s + 16384.0) * (double)std::max<int64_t>(waves, 8);
+        const double t = ((double)Nr / (double)s + warm) * (double)std::max<int64_t>(waves, 8);
         if (t < best_t * (1.0 - 1e-9)) {
             best_t = t;
             best = (int)s;
@@ -787,7 +844,21 @@ KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
     l.KC = pick_kc(k);
     l.mfma = l.exp;  // every expanded-form screen runs on the matrix cores
 
-    l.nsplit = l.mfma ? pick_nsplit_mfma(Nr, Nq, dsp::mq_qpb(l.KC), device_cus())
+    // seeded thresholds (matrix-core screen, reference sets of >= KNN_SEED_MIN_NR rows): a pilot
+    // screen over every rstride-th row (~KNN_SEED_SAMPLE rows) seeds each query's threshold
+    l.rstride = 0;
+    l.nsample = 0;
+    l.nsplit_p = 0;
+    if (l.mfma && Nr >= KNN_SEED_MIN_NR) {
+        l.rstride = (int)std::max<int64_t>(2, Nr / KNN_SEED_SAMPLE);
+        l.nsample = (int)((Nr + l.rstride - 1) / l.rstride);
+    }
+#ifdef DSP_KNN_DIAG  // diagnostic build only: seeding off (DSP_KNN_SEED=0)
+    if (const char *e = getenv("DSP_KNN_SEED"))
+        if (atoi(e) == 0) l.rstride = l.nsample = 0;
+#endif
+    l.nsplit = l.mfma ? pick_nsplit_mfma(Nr, Nq, dsp::mq_qpb(l.KC), device_cus(),
+                                         l.rstride ? KNN_SEED_WARM : 16384.0)
                       : pick_nsplit(Nr, Nq, l.hd ? dsp::KNN_TQ : dsp::KNN_TQ * dsp::KNN_QP);
 #ifdef DSP_KNN_DIAG  // diagnostic build only: forced split count (tools/knn_split_sweep.sh)
     if (const char *e = getenv("DSP_KNN_NSPLIT")) l.nsplit = std::max(1, std::min(64, atoi(e)));
@@ -806,6 +877,15 @@ KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
     l.cand_d = o; o += al((size_t)l.nsplit * Nq * l.KC * 4);
     l.cand_i = o; o += al((size_t)l.nsplit * Nq * l.KC * 4);
     l.misc = o;  o += al(16 + (size_t)Nq * 4);   // maxnorm bits, fallback count, fallback list
+    l.pilot_d = l.seed = 0;
+    if (l.rstride) {
+        // pilot splits: enough workgroups to fill the chip twice over, >= one tile of rows each
+        const int64_t qblocks = (Nq + dsp::mq_qpb(l.KC) - 1) / dsp::mq_qpb(l.KC);
+        l.nsplit_p = (int)std::max<int64_t>(1, std::min<int64_t>({(2 * device_cus() + qblocks - 1) / qblocks,
+                                                                  (l.nsample + dsp::MQ_TR - 1) / dsp::MQ_TR, 64}));
+        l.pilot_d = o; o += al((size_t)l.nsplit_p * Nq * l.KC * 4);
+        l.seed = o;    o += al((size_t)Nq * 4);
+    }
     l.total = o;
     return l;
 }
@@ -822,7 +902,8 @@ void launch_screen(dim3 g, hipStream_t s, const float *r, int64_t Nr, const floa
 template <int KC>
 bool launch_merge(hipStream_t s, const double *ref, const double *query, int64_t Nr, int64_t Nq, int D, int k,
                   int nsplit, int64_t self, const float *cd, const int *ci, const unsigned *mx, double er,
-                  double ea, const int32_t *lbl, int32_t *idx, double *dist, int32_t *pred, int *fbc, int *fbl)
+                  double ea, const int32_t *lbl, int32_t *idx, double *dist, int32_t *pred, int *fbc, int *fbl,
+                  const float *seed)
 {
     // 64-thread workgroups: 12 500 queries (one rank of the 8-GPU self-query) are 196 of them
     const dim3 g((unsigned)((Nq + 63) / 64)), b(64);
@@ -830,19 +911,19 @@ bool launch_merge(hipStream_t s, const double *ref, const double *query, int64_t
     if (k > KC) return false;
     if (k <= 8) {
         hipLaunchKernelGGL((dsp::knn_merge<KC, 8>), g, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self, cd, ci, mx,
-                           er, ea, lbl, idx, dist, pred, fbc, fbl);
+                           er, ea, lbl, idx, dist, pred, fbc, fbl, seed);
         return true;
     }
     if constexpr (KC >= 16) {
         if (k <= 16) {
             hipLaunchKernelGGL((dsp::knn_merge<KC, 16>), g, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self, cd, ci,
-                               mx, er, ea, lbl, idx, dist, pred, fbc, fbl);
+                               mx, er, ea, lbl, idx, dist, pred, fbc, fbl, seed);
             return true;
         }
     }
     if constexpr (KC >= 24) {
         hipLaunchKernelGGL((dsp::knn_merge<KC, 32>), g, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self, cd, ci,
-                           mx, er, ea, lbl, idx, dist, pred, fbc, fbl);
+                           mx, er, ea, lbl, idx, dist, pred, fbc, fbl, seed);
         return true;
     }
     return false;
@@ -877,6 +958,12 @@ extern "C" size_t dsp_knn_workspace_bytes(int64_t Nr, int64_t Nq, int D, int k)
     return knn_layout(Nr, Nq, D, k).total;
 }
 
+extern "C" size_t dsp_knn_workspace_fallbacks_offset(int64_t Nr, int64_t Nq, int D, int k)
+{
+    if (Nr < 0 || Nq < 0 || D < 1 || D > KNN_DMAX || k < 1 || k > 32) return 0;
+    return knn_layout(Nr, Nq, D, k).misc + 4;
+}
+
 extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, int64_t Nr,
                                 const double *query, int64_t Nq, int D, int k, int64_t self_offset,
                                 int n_classes, int32_t *idx, double *dist, int32_t *pred,
@@ -898,6 +985,7 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
     unsigned *mx = (unsigned *)(ws + l.misc);
     int *fbc = (int *)(ws + l.misc + 4);
     int *fbl = (int *)(ws + l.misc + 16);
+    float *seedp = l.rstride ? (float *)(ws + l.seed) : nullptr;
     if (hipMemsetAsync(ws + l.misc, 0, 16, s) != hipSuccess) return DSP_ERR_HIP;
     const int cb = 256;
     if (Nr > 0)
@@ -918,16 +1006,38 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
         }
     } else if (l.mfma) {
         const int qpb = dsp::mq_qpb(l.KC);
-        const dim3 g((unsigned)((Nq + qpb - 1) / qpb), (unsigned)l.nsplit), b(64 * dsp::MQ_W);
-#define DSP_SCREEN_MQ(DPV, KCV)                                                                   \
+        const unsigned qb = (unsigned)((Nq + qpb - 1) / qpb);
+        const dim3 b(64 * dsp::MQ_W);
+#define DSP_SCREEN_MQ(DPV, KCV, G, NR, NS, CD, CI, RSTR, SEED)                                     \
     if (l.DP == DPV && l.KC == KCV)                                                               \
-    hipLaunchKernelGGL((dsp::knn_screen_mfma<DPV, KCV>), g, b, 0, s, ref32, Nr, q32, Nq, self_offset, \
-                       l.nsplit, cd, ci)
-        DSP_SCREEN_MQ(16, 8); DSP_SCREEN_MQ(16, 16); DSP_SCREEN_MQ(16, 24); DSP_SCREEN_MQ(16, 36);
-        DSP_SCREEN_MQ(32, 8); DSP_SCREEN_MQ(32, 16); DSP_SCREEN_MQ(32, 24); DSP_SCREEN_MQ(32, 36);
-#if KNN_MFMA_KC6
-        DSP_SCREEN_MQ(16, 6); DSP_SCREEN_MQ(32, 6);
+    hipLaunchKernelGGL((dsp::knn_screen_mfma<DPV, KCV>), G, b, 0, s, ref32, NR, q32, Nq, self_offset, NS, \
+                       CD, CI, RSTR, SEED)
+#define DSP_SCREEN_MQ_ALL(...)                                                                    \
+        DSP_SCREEN_MQ(16, 8, __VA_ARGS__); DSP_SCREEN_MQ(16, 16, __VA_ARGS__); DSP_SCREEN_MQ(16, 24, __VA_ARGS__); \
+        DSP_SCREEN_MQ(16, 36, __VA_ARGS__); DSP_SCREEN_MQ(32, 8, __VA_ARGS__); DSP_SCREEN_MQ(32, 16, __VA_ARGS__); \
+        DSP_SCREEN_MQ(32, 24, __VA_ARGS__); DSP_SCREEN_MQ(32, 36, __VA_ARGS__); DSP_SCREEN_MQ(16, 6, __VA_ARGS__); \
+        DSP_SCREEN_MQ(32, 6, __VA_ARGS__)
+        if (l.rstride) {
+            float seed_scale = 1.f;
+#ifdef DSP_KNN_DIAG  // diagnostic build only: an adversarially tight seed (fallback tests)
+            if (const char *e = getenv("DSP_KNN_SEED_SCALE")) seed_scale = (float)atof(e);
 #endif
+            // pilot over the sampled rows (same kernel, same fp32 arithmetic), then the seeds
+            float *pd = (float *)(ws + l.pilot_d);
+            const dim3 gp(qb, (unsigned)l.nsplit_p);
+            DSP_SCREEN_MQ_ALL(gp, (int64_t)l.nsample, l.nsplit_p, pd, (int *)nullptr, l.rstride, (const float *)nullptr);
+            const dim3 gs((unsigned)((Nq + 255) / 256));
+            switch (l.KC) {
+            case 6: hipLaunchKernelGGL((dsp::knn_seed<6>), gs, dim3(256), 0, s, pd, l.nsplit_p, Nq, seedp, seed_scale); break;
+            case 8: hipLaunchKernelGGL((dsp::knn_seed<8>), gs, dim3(256), 0, s, pd, l.nsplit_p, Nq, seedp, seed_scale); break;
+            case 16: hipLaunchKernelGGL((dsp::knn_seed<16>), gs, dim3(256), 0, s, pd, l.nsplit_p, Nq, seedp, seed_scale); break;
+            case 24: hipLaunchKernelGGL((dsp::knn_seed<24>), gs, dim3(256), 0, s, pd, l.nsplit_p, Nq, seedp, seed_scale); break;
+            default: hipLaunchKernelGGL((dsp::knn_seed<36>), gs, dim3(256), 0, s, pd, l.nsplit_p, Nq, seedp, seed_scale); break;
+            }
+        }
+        const dim3 g(qb, (unsigned)l.nsplit);
+        DSP_SCREEN_MQ_ALL(g, Nr, l.nsplit, cd, ci, 1, (const float *)seedp);
+#undef DSP_SCREEN_MQ_ALL
 #undef DSP_SCREEN_MQ
     } else {
         const dim3 g((unsigned)((Nq + dsp::KNN_TQ * dsp::KNN_QP - 1) / (dsp::KNN_TQ * dsp::KNN_QP)), (unsigned)l.nsplit);
@@ -944,12 +1054,12 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
     bool merged = false;
     switch (l.KC) {
 #if KNN_MFMA_KC6
-    case 6: merged = launch_merge<6>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
+    case 6: merged = launch_merge<6>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl, seedp); break;
 #endif
-    case 8: merged = launch_merge<8>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
-    case 16: merged = launch_merge<16>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
-    case 24: merged = launch_merge<24>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
-    default: merged = launch_merge<36>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl); break;
+    case 8: merged = launch_merge<8>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl, seedp); break;
+    case 16: merged = launch_merge<16>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl, seedp); break;
+    case 24: merged = launch_merge<24>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl, seedp); break;
+    default: merged = launch_merge<36>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl, seedp); break;
     }
     if (!merged) return DSP_ERR_ARGS;  // unreachable while KC >= k + KNN_SLACK (knn_layout)
     const unsigned fbgrid = (unsigned)(Nq < 512 ? Nq : 512);

@@ -27,7 +27,7 @@ CLIP_FLAG_VAD_EXACT = 0x100
 ABI_VERSION = 2  # include/dsp_audiorec.h DSP_ABI_VERSION this binding is typed for
 
 EXPORTS = ("dsp_extract_lds_bytes", "dsp_extract_features", "dsp_extract_general_workspace_bytes",
-           "dsp_extract_general", "dsp_knn_workspace_bytes",
+           "dsp_extract_general", "dsp_knn_workspace_bytes", "dsp_knn_workspace_fallbacks_offset",
            "dsp_knn_classify", "dsp_zscore_fit", "dsp_zscore_apply", "dsp_abi_version")
 
 _lib = None
@@ -66,6 +66,8 @@ def load_library(path=LIB_PATH):
                                       vp, vp, vp, vp, vp, vp, i32, vp, i32, vp, sz, vp]
     L.dsp_knn_workspace_bytes.restype = sz
     L.dsp_knn_workspace_bytes.argtypes = [i64, i64, i32, i32]
+    L.dsp_knn_workspace_fallbacks_offset.restype = sz
+    L.dsp_knn_workspace_fallbacks_offset.argtypes = [i64, i64, i32, i32]
     L.dsp_knn_classify.restype = i32
     L.dsp_knn_classify.argtypes = [vp, vp, i64, vp, i64, i32, i32, i64, i32, vp, vp, vp, vp, sz, vp]
     L.dsp_zscore_fit.restype = i32

@@ -174,11 +174,13 @@ def process_audio_batch(pcm, offsets=None, frame_length=1102, frame_shift=441, w
     return dict(fx(pcm, offsets, max_len))
 
 
-def knn_classify(ref, ref_labels, query, k, self_offset=-1, n_classes=None, with_pred=True):
+def knn_classify(ref, ref_labels, query, k, self_offset=-1, n_classes=None, with_pred=True, stats=None):
     """Exact k-NN (KNeighborsClassifier semantics) on the device.
 
     ref [Nr, D] / query [Nq, D] float64 (cast if needed), ref_labels int [Nr].
-    Returns (idx int32 [Nq,k], dist float64 [Nq,k], pred int32 [Nq] or None).
+    Returns (idx int32 [Nq,k], dist float64 [Nq,k], pred int32 [Nq] or None).  A dict passed as
+    ``stats`` receives "fallbacks": the queries answered by the exhaustive fp64 fallback (one host
+    sync).
     """
     import torch
     d = _hip.require_device()
@@ -200,6 +202,9 @@ def knn_classify(ref, ref_labels, query, k, self_offset=-1, n_classes=None, with
                                      int(self_offset), int(n_classes), _hip.ptr(idx), _hip.ptr(dist),
                                      _hip.ptr(pred), _hip.ptr(ws), ws_bytes, _hip.stream_handle(d))
     _hip.check(rc, "dsp_knn_classify")
+    if stats is not None and Nq > 0:
+        off = _hip.lib().dsp_knn_workspace_fallbacks_offset(Nr, Nq, D, k)
+        stats["fallbacks"] = int(ws[off:off + 4].view(torch.int32).item())
     return idx, dist, pred
 
 

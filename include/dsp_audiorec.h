@@ -158,6 +158,9 @@ int dsp_extract_general(const void *pcm, int sample_bytes, const int64_t *offset
  * D > 32 (the sequence method's flattened features): dimensions walked in chunks of 16.
  */
 size_t dsp_knn_workspace_bytes(int64_t Nr, int64_t Nq, int D, int k);
+/* Diagnostic: byte offset in that workspace of an int32 that dsp_knn_classify leaves holding the
+ * number of queries the screen could not certify (answered by the exhaustive fp64 fallback). */
+size_t dsp_knn_workspace_fallbacks_offset(int64_t Nr, int64_t Nq, int D, int k);
 int dsp_knn_classify(const double *ref, const int32_t *ref_labels, int64_t Nr, const double *query,
                      int64_t Nq, int D, int k, int64_t self_offset, int n_classes, int32_t *idx,
                      double *dist, int32_t *pred, void *workspace, size_t workspace_bytes,

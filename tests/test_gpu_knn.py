@@ -160,3 +160,94 @@ def test_knn_configs4_rank_shard_at_size():
         i0, d0, p0 = oracle.knn(X, y, X[a:a + 500], k, n_classes=10, self_offset=a, nthreads=16)
         assert np.array_equal(iA[a:a + 500].cpu().numpy(), i0) and np.array_equal(dA[a:a + 500].cpu().numpy(), d0)
         assert np.array_equal(pA[a:a + 500].cpu().numpy(), p0)
+
+
+def _with_library(name, fn):
+    """Run fn() with src._hip bound to lib/libdsp_audiorec_<name>.so (a diagnostic build)."""
+    import os
+    from src import _hip
+    path = os.path.join(os.path.dirname(_hip.LIB_PATH), "libdsp_audiorec_%s.so" % name)
+    saved = _hip._lib
+    _hip._lib = None
+    try:
+        _hip.load_library(path)
+        return fn()
+    finally:
+        _hip._lib = saved
+
+
+@pytest.mark.parametrize("k", [3, 5])
+def test_knn_seeded_screen_vs_oracle(k):
+    """Reference sets of >= 32k rows seed every query's screening threshold from a pilot screen of
+    every rstride-th row (knn_seed).  Indices, fp64 distances and votes bit-exact against the
+    oracle, for a self-query block and foreign queries; the seed must be loose enough that almost
+    no query needs the fallback."""
+    from src.pipeline import knn_classify
+    rng = np.random.default_rng(50 + k)
+    X, y = _clustered(rng, 50000, 15)
+    Q, _ = _clustered(rng, 2000, 15)
+    st = {}
+    i1, d1, p1 = knn_classify(X, y, Q, k, stats=st)
+    i0, d0, p0 = oracle.knn(X, y, Q, k, n_classes=10, nthreads=16)
+    assert np.array_equal(i1.cpu().numpy(), i0) and np.array_equal(d1.cpu().numpy(), d0)
+    assert np.array_equal(p1.cpu().numpy(), p0)
+    assert st["fallbacks"] <= 20, st
+    lo = 31000
+    i1, d1, p1 = knn_classify(X, y, X[lo:lo + 2000], k, self_offset=lo)
+    i0, d0, p0 = oracle.knn(X, y, X[lo:lo + 2000], k, n_classes=10, self_offset=lo, nthreads=16)
+    assert np.array_equal(i1.cpu().numpy(), i0) and np.array_equal(d1.cpu().numpy(), d0)
+    assert np.array_equal(p1.cpu().numpy(), p0)
+
+
+def test_knn_adversarially_tight_seed_falls_back_exactly(monkeypatch):
+    """The diagnostic build scales every seed by DSP_KNN_SEED_SCALE: at 0.25 the seeds sit below
+    the true k-th distance, the screen keeps too few rows, certification fails, and the exhaustive
+    fallback must still return the oracle's exact answer (self-query and foreign queries)."""
+    from src.pipeline import knn_classify
+    rng = np.random.default_rng(77)
+    X, y = _clustered(rng, 40000, 15)
+    Q, _ = _clustered(rng, 600, 15)
+    monkeypatch.setenv("DSP_KNN_SEED_SCALE", "0.25")
+
+    def run():
+        st1, st2 = {}, {}
+        a = knn_classify(X, y, Q, 5, stats=st1)
+        b = knn_classify(X, y, X[100:700], 5, self_offset=100, stats=st2)
+        return a, b, st1, st2
+    (i1, d1, p1), (j1, e1, q1), st1, st2 = _with_library("knndiag", run)
+    assert st1["fallbacks"] > 300 and st2["fallbacks"] > 300, (st1, st2)
+    i0, d0, p0 = oracle.knn(X, y, Q, 5, n_classes=10, nthreads=16)
+    assert np.array_equal(i1.cpu().numpy(), i0) and np.array_equal(d1.cpu().numpy(), d0)
+    assert np.array_equal(p1.cpu().numpy(), p0)
+    j0, e0, q0 = oracle.knn(X, y, X[100:700], 5, n_classes=10, self_offset=100, nthreads=16)
+    assert np.array_equal(j1.cpu().numpy(), j0) and np.array_equal(e1.cpu().numpy(), e0)
+    assert np.array_equal(q1.cpu().numpy(), q0)
+
+
+def test_knn_kc6_duplicates_and_ties_fall_back_exactly():
+    """k = 5 on splits of <= 32k rows screens six candidates per split (slack 1).  Many exact
+    duplicate rows and equidistant rows make the screened lists tie at their last entry, so
+    certification must fail for those queries and the fallback decide them: bit-exact against the
+    oracle with and without the self-query exclusion, and some queries must have fallen back."""
+    from src.pipeline import knn_classify
+    rng = np.random.default_rng(31)
+    base = rng.standard_normal((400, 15))
+    X = np.repeat(base, 25, axis=0)  # 10 000 rows, each value 25 times
+    # equidistant rows: +-e_j shifts of one centre
+    c = rng.standard_normal(15)
+    ring = np.concatenate([c + 0.5 * np.eye(15), c - 0.5 * np.eye(15)])
+    X = np.concatenate([X, np.repeat(ring, 4, axis=0)])
+    y = rng.integers(0, 10, X.shape[0]).astype(np.int32)
+    Q = np.concatenate([base[:300] + 1e-9, np.repeat(c[None], 20, axis=0)])
+    st = {}
+    i1, d1, p1 = knn_classify(X, y, Q, 5, stats=st)
+    i0, d0, p0 = oracle.knn(X, y, Q, 5, n_classes=10, nthreads=16)
+    assert np.array_equal(i1.cpu().numpy(), i0) and np.array_equal(d1.cpu().numpy(), d0)
+    assert np.array_equal(p1.cpu().numpy(), p0)
+    assert st["fallbacks"] > 0, st
+    st = {}
+    i1, d1, p1 = knn_classify(X, y, X[:500], 5, self_offset=0, stats=st)
+    i0, d0, p0 = oracle.knn(X, y, X[:500], 5, n_classes=10, self_offset=0, nthreads=16)
+    assert np.array_equal(i1.cpu().numpy(), i0) and np.array_equal(d1.cpu().numpy(), d0)
+    assert np.array_equal(p1.cpu().numpy(), p0)
+    assert st["fallbacks"] > 0, st
