@@ -722,9 +722,15 @@ __device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur
 // sits in the buffer and equal dsp_extract_general's.  Per sample y = w_j x (the reference's
 // windowed frame, :329-331), E += y^2, M += |y|; the weights of a vector's 8 samples are two
 // aligned 16-B reads from the window copy shifted by fs mod 4.  Frame group g of 4 frames goes to
-// the wave whose rank (wrank, 0 .. NWAVE-1) is g mod NWAVE.  Returns F.
+// the wave whose rank (wrank, 0 .. NWAVE-1) is g mod NWAVE.  between() runs after the wave's first
+// batch of crop loads is issued and before it is used (other work hides the L2 latency).  Returns F.
+struct Nothing {
+    __device__ void operator()() const {}
+};
+template <typename Between = Nothing>
 __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int st, int en,
-                                         const ClipStats &cs, int j0, int j1, int wrank, int lane)
+                                         const ClipStats &cs, int j0, int j1, int wrank, int lane,
+                                         Between between = Nothing())
 {
     const int L = p.L, S = p.S, n = cur.n, lead = cur.lead;
     const int m = en - st;  // > 0 always (start < end)
@@ -756,11 +762,24 @@ __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, c
     };
     constexpr int R4_KV = EXTRACT_R4_KV;  // vectors per lane in one batch
     const int rl = lane & 15, row = lane >> 4;
-    for (int gi = wrank; !(DSP_ABL & 1) && 4 * gi < F; gi += NWAVE) {
+    auto frame_start = [&](int gi) {  // (sample coords) of this lane's row frame in group gi
+        const int g = 4 * gi + row;
+        return st + (g < F ? g : F - 1) * S;
+    };
+    // the first batch of the wave's first group, issued before between()
+    short8 xv[R4_KV];
+    const bool any = !(DSP_ABL & 1) && 4 * wrank < F;
+    if (any) {
+        const int va = frame_start(wrank) >> 3;
+#pragma unroll
+        for (int k = 0; k < R4_KV; k++) xv[k] = load_cvec(p, cur, va + rl + 16 * k);
+    }
+    between();
+    bool first = true;
+    for (int gi = wrank; any && 4 * gi < F; gi += NWAVE) {
         const int g = 4 * gi + row;
         const bool act = g < F;
-        const int gc = act ? g : F - 1;
-        const int fs = st + gc * S;
+        const int fs = frame_start(gi);
         const int lim = min(L, en - fs);  // samples beyond the crop are zero padding
         const bool padded = lim < L;
         const int va = fs >> 3, vb = (fs + lim - 1) >> 3;
@@ -769,9 +788,10 @@ __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, c
         float2v ea = {0.f, 0.f};
         float m0 = 0.f, m1 = 0.f;
         for (int v0 = va; v0 <= vb; v0 += 16 * R4_KV) {
-            short8 xv[R4_KV];
+            if (!first)
 #pragma unroll
-            for (int k = 0; k < R4_KV; k++) xv[k] = load_cvec(p, cur, v0 + rl + 16 * k);
+                for (int k = 0; k < R4_KV; k++) xv[k] = load_cvec(p, cur, v0 + rl + 16 * k);
+            first = false;
             if (vfix >= 0)  // clip-uniform, rare
 #pragma unroll
                 for (int k = 0; k < R4_KV; k++)
@@ -1454,10 +1474,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
         __syncthreads();  // B2
 
         // ---- S3 --------------------------------------------------------------------------------
-        if (okB && sb.nv > 0) vad_frames_fast(cB, rb, L, S, sb, qa, pa_w, pa_e0, pa_e1, tid);
-        STAMP(ib >= 0 ? ib : 0, 7);
+        // A's first crop loads go out first; B's VAD frames (LDS work) run under their latency
+        auto vadB = [&]() {
+            if (okB && sb.nv > 0) vad_frames_fast(cB, rb, L, S, sb, qa, pa_w, pa_e0, pa_e1, tid);
+        };
         int F = 0;
-        if (actA) F = r4_frames(p, cA, ra, st, en, sa, j0, j1, NWAVE - 1 - wid, lane);  // waves 7, 6, .. first
+        if (actA)
+            F = r4_frames(p, cA, ra, st, en, sa, j0, j1, NWAVE - 1 - wid, lane, vadB);  // waves 7, 6, .. first
+        else
+            vadB();
         STAMP(ia >= 0 ? ia : 0, 12);
         __syncthreads();  // B3
 
