@@ -62,6 +62,12 @@ static constexpr int NRV = 4 * RREG;       // 16-B vectors per thread in registe
     } while (0)
 // per workgroup (row blockIdx.x, slots 16..): real-time and shader-clock stamps (WG_STAMP, at
 // entry and exit) and shader-clock stamps inside the prologue (WG_CK)
+// the pipelined kernel: lane 0 of wave w stamps slot k of clip row `clip`
+#define STAMPW(clip, k, w)                                                                       \
+    do {                                                                                         \
+        if (threadIdx.x == 64 * (w) && p.stamps && (clip) >= 0)                                  \
+            p.stamps[(size_t)(clip) * 32 + (k)] = __builtin_amdgcn_s_memtime();                  \
+    } while (0)
 #define WG_STAMP(k)                                                                          \
     do {                                                                                     \
         if (threadIdx.x == 0 && p.stamps) {                                                  \
@@ -82,6 +88,9 @@ static constexpr int NRV = 4 * RREG;       // 16-B vectors per thread in registe
     } while (0)
 #define STAMP(clip, k) \
     do {               \
+    } while (0)
+#define STAMPW(clip, k, w) \
+    do {                   \
     } while (0)
 #endif
 
@@ -1401,7 +1410,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
         cA.posw = slotB ? posw0 : posw1;
         cB.sh = shB;
         cB.posw = slotB ? posw1 : posw0;
-        STAMP(ib >= 0 ? ib : 0, 0);
+        // diagnostic stamps (make stamps), row of the trip's clip B: 0 trip start, 11 A's scan done,
+        // 1 S1 done, 2 S2 done, 12 / 14 S3 done on wave 7 / 0, 15 A's R5 (wave 0) done, 8 B's p90
+        // done (wave 6), 3 S4 done
+        STAMPW(ib, 0, 0);
 
         // ---- S1 --------------------------------------------------------------------------------
         if (tid == 0) {
@@ -1419,6 +1431,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
             const int flag = vad_scan<true, true>(p, cA, sa.nv, lane);
             if (lane == 0) shA->exact = sa.Mp > 0.0 ? flag : 0;
             __builtin_amdgcn_s_setprio(0);
+            STAMPW(ib, 11, 0);
         }
         if (okB) {
             R1Acc acc = r1_acc_init();
@@ -1430,7 +1443,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
             }
             r1_reduce(acc, shB, wid, lane);
         }
-        STAMP(ib >= 0 ? ib : 0, 1);
+        STAMPW(ib, 1, 0);
         __syncthreads();  // B1
 
         // ---- S2 --------------------------------------------------------------------------------
@@ -1470,7 +1483,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
         }
         inext = uni(shs0->next);
         rnext = inext >= 0 ? clip_ref(p, inext) : clip_none();
-        STAMP(ib >= 0 ? ib : 0, 2);
+        STAMPW(ib, 2, 0);
         __syncthreads();  // B2
 
         // ---- S3 --------------------------------------------------------------------------------
@@ -1483,7 +1496,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
             F = r4_frames(p, cA, ra, st, en, sa, j0, j1, NWAVE - 1 - wid, lane, vadB);  // waves 7, 6, .. first
         else
             vadB();
-        STAMP(ia >= 0 ? ia : 0, 12);
+        STAMPW(ib, 12, NWAVE - 1);
+        STAMPW(ib, 14, 0);
         __syncthreads();  // B3
 
         // ---- S4 --------------------------------------------------------------------------------
@@ -1506,17 +1520,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
                 p.status[ia] = DSP_CLIP_OK;
             }
         }
-        STAMP(ia >= 0 ? ia : 0, 9);
+        STAMPW(ib, 15, 0);
         if (okB && sb.nv > 0) {
             if (wid == NWAVE - 2) {  // p90 order statistics (:198), then the scan: critical path
                 __builtin_amdgcn_s_setprio(2);
                 p90_select_wave(cB, sb.nv, lane);
                 __builtin_amdgcn_s_setprio(0);
+                STAMPW(ib, 8, NWAVE - 2);
             } else if (wid == NWAVE - 1) {
                 vad_noise(cB, sb.nv, lane);
             }
         }
-        STAMP(ib >= 0 ? ib : 0, 3);
+        STAMPW(ib, 3, 0);
         __syncthreads();  // B4
     }
     if (threadIdx.x == 0) queue_done(p);

@@ -15,4 +15,5 @@ bash tools/ab_bench.sh 100000 r03 pipe0 base > $O/ab100k.txt 2>&1; cat $O/ab100k
 for nq in 12500 100000; do
   timeout -k 10 200 python3 tools/bench_knn.py --no-cpu --queries $nq > $O/knn_$nq.json; cat $O/knn_$nq.json
 done
+bash tools/stamps_run.sh $T 100000 || true
 echo DONE
