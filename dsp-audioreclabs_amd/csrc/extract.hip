@@ -894,7 +894,7 @@ __device__ __forceinline__ void r5_fast(const Ctx &c, int F, float *featb, int w
 // at most 128 VAD and feature frames, so the long-clip paths drop out
 template <bool EXACT, bool FAST>
 __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, int i, const ClipRef &cur,
-                                          short8 (&regs)[NRV], unsigned claim = 0x7fffffffu)
+                                          short8 (&regs)[NRV], int claim = -1)
 {
     Shared *sh = c.sh;
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
@@ -1103,13 +1103,13 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     if (!FAST && F > 128)
         for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
     if constexpr (!EXACT)
-        if (tid == 0) sh->next = (int)min(claim, 0x7fffffffu);  // claimed at the clip's start
+        if (tid == 0) sh->next = claim;  // claimed at the clip's start (-1: none)
     __syncthreads();
     if constexpr (!EXACT) {
         // regs are dead since R2: the next clip's words load while R5 runs (unconditional, a
         // clip_none() reads zeros, so the compiler's vmcnt bookkeeping stays exact)
         const int nx = sh->next;
-        issue_clip(regs, p, nx < p.B ? clip_ref(p, nx) : clip_none());
+        issue_clip(regs, p, nx >= 0 ? clip_ref(p, nx) : clip_none());
     }
     STAMP(i, 5);
 
@@ -1270,26 +1270,67 @@ __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &
     __syncthreads();
 }
 
-// Clips: blockIdx.x first, then clips claimed from the caller's launch-wide counter (p.queue), so
-// that workgroups whose clips run short take more of them (a static i, i + G, ... split ends on the
-// slowest workgroup: 3.19-3.98 ms spread at 100 000 clips); without a counter, the static split.
-// Thread 0 only.
-__device__ __forceinline__ unsigned claim_clip(const ExtractParams &p, unsigned &cursor)
+// Clip queue (ABI 3).  p.queue: the caller's zeroed 64-byte scratch, words 0-7 the claim counters
+// of eight ranges of clip chunks (EXTRACT_CHUNK consecutive clips each; range x = the chunks
+// [x nch / 8, (x + 1) nch / 8)), word 8 the count of workgroups done.  A workgroup claims chunks
+// from the range of the XCD it runs on (HW_REG_XCC_ID: placement is a performance matter only,
+// any id is correct), then from the others in turn once its own is exhausted: one atomic per chunk
+// instead of per clip, consecutive clips on one XCD -- their 76-B output rows share cache lines in
+// that XCD's L2 instead of leaving it as partial-line writes -- and fast workgroups take more
+// chunks (a static i, i + G, ... split ends on the slowest workgroup: 3.19-3.98 ms spread at
+// 100 000 clips).  p.queue == NULL: the static split.  Thread 0 only.
+#ifndef EXTRACT_CHUNK
+#define EXTRACT_CHUNK 4
+#endif
+struct ClipQueue {
+    unsigned *q;
+    int B, nch, xcd;
+    int next, end;  // the current chunk's next clip and its end
+    int cursor;     // static split
+};
+__device__ __forceinline__ ClipQueue queue_open(const ExtractParams &p)
 {
-    if (p.queue)
-        return gridDim.x + __hip_atomic_fetch_add(p.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    cursor += gridDim.x;
-    return cursor;
+    ClipQueue Q;
+    Q.q = p.queue;
+    Q.B = p.B;
+    Q.nch = (p.B + EXTRACT_CHUNK - 1) / EXTRACT_CHUNK;
+    Q.xcd = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;  // HW_REG_XCC_ID[3:0]
+    Q.next = Q.end = 0;
+    Q.cursor = (int)blockIdx.x - (int)gridDim.x;
+    return Q;
+}
+// the next clip of this workgroup, -1 when none is left
+__device__ __forceinline__ int queue_next(ClipQueue &Q)
+{
+    if (!Q.q) {
+        Q.cursor += gridDim.x;
+        return Q.cursor < Q.B ? Q.cursor : -1;
+    }
+    if (Q.next < Q.end) return Q.next++;
+    for (int t = 0; t < 8; t++) {
+        const int y = (Q.xcd + t) & 7;
+        const unsigned c0 = (unsigned)(y * Q.nch / 8), c1 = (unsigned)((y + 1) * Q.nch / 8);
+        // a relaxed look first: exhausted ranges cost no atomic
+        if (c0 + __hip_atomic_load(Q.q + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= c1) continue;
+        const unsigned c = c0 + __hip_atomic_fetch_add(Q.q + y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c < c1) {
+            Q.next = (int)c * EXTRACT_CHUNK;
+            Q.end = min(Q.B, Q.next + EXTRACT_CHUNK);
+            return Q.next++;
+        }
+    }
+    return -1;
 }
 // the last workgroup out resets the queue for the next launch on the stream: every claim of every
 // workgroup precedes its increment of the done count.  Thread 0 only.
 __device__ __forceinline__ void queue_done(const ExtractParams &p)
 {
     if (!p.queue) return;
-    const unsigned d = __hip_atomic_fetch_add(p.queue + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned d = __hip_atomic_fetch_add(p.queue + 8, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (d == gridDim.x - 1) {
-        __hip_atomic_store(p.queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(p.queue + 1, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int y = 0; y < 8; y++) __hip_atomic_store(p.queue + y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p.queue + 8, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1309,26 +1350,28 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     WG_STAMP(16);
     build_window(p, c, tid, lane, wid);
+    ClipQueue Q = queue_open(p);
+    if (tid == 0) sh->next = queue_next(Q);
+    __syncthreads();
     short8 regs[NRV];
     bool inflight = false;  // regs already hold clip i's loads (issued by the previous clip's R4)
-    unsigned cursor = blockIdx.x;
-    for (int i = blockIdx.x; i < p.B;) {
+    for (int i = sh->next; i >= 0;) {
         const ClipRef cur = clip_ref(p, i);
-        unsigned claim = 0x7fffffffu;
+        int claim = -1;
         if (!cur.ok) {
             __syncthreads();  // everyone has read sh->next (the ok path has barriers in clip_body)
-            if (tid == 0) claim = claim_clip(p, cursor);
+            if (tid == 0) claim = queue_next(Q);
             write_bad_clip(p, i, tid);
             inflight = false;
         } else {
             if (!inflight) issue_clip(regs, p, cur);
-            if (tid == 0) claim = claim_clip(p, cursor);
+            if (tid == 0) claim = queue_next(Q);
             c.stamp_clip = i;
             const bool done = clip_body<false, false>(p, c, i, cur, regs, claim);
             if (!done && tid == 0) p.status[i] = DSP_CLIP_UNCERTIFIED;
             inflight = done;  // a deferred clip returns before R4
         }
-        if (tid == 0) sh->next = (int)min(claim, 0x7fffffffu);
+        if (tid == 0) sh->next = claim;
         __syncthreads();  // LDS summaries are rewritten by the next clip; sh->next published
         i = sh->next;
     }
@@ -1377,8 +1420,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     build_window(p, c0, (int)threadIdx.x, (int)threadIdx.x & 63, wid);
     const int j0 = uni(shs0->j0), j1 = uni(shs0->j1);
 
-    unsigned cursor = blockIdx.x;
-    int inext = (int)blockIdx.x < p.B ? (int)blockIdx.x : -1;  // the clip whose words are in flight
+    ClipQueue Q = queue_open(p);
+    if (threadIdx.x == 0) shs0->next = queue_next(Q);
+    __syncthreads();
+    int inext = uni(shs0->next);  // the clip whose words are in flight
     ClipRef rnext = inext >= 0 ? clip_ref(p, inext) : clip_none();
     short8 regs[NRV];
     issue_clip_pipe(regs, p, rnext, (int)threadIdx.x);
@@ -1416,14 +1461,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
         STAMPW(ib, 0, 0);
 
         // ---- S1 --------------------------------------------------------------------------------
-        if (tid == 0) {
-            int nx = -1;
-            if (ib >= 0) {
-                const unsigned cl = claim_clip(p, cursor);
-                nx = cl < (unsigned)p.B ? (int)cl : -1;
-            }
-            shs0->next = nx;
-        }
+        if (tid == 0) shs0->next = ib >= 0 ? queue_next(Q) : -1;
         if (wid == 0 && okA && sa.nv > 0) {
             // the scan is the trip's single-wave critical path: issue priority over the
             // co-resident workgroup's waves

@@ -24,7 +24,8 @@ CLIP_NO_FRAMES = 3
 CLIP_TOO_LONG = 4
 CLIP_UNCERTIFIED = 5  # reserved (never produced)
 CLIP_FLAG_VAD_EXACT = 0x100
-ABI_VERSION = 2  # include/dsp_audiorec.h DSP_ABI_VERSION this binding is typed for
+ABI_VERSION = 3  # include/dsp_audiorec.h DSP_ABI_VERSION this binding is typed for
+QUEUE_WS_BYTES = 64  # DSP_QUEUE_WS_BYTES
 
 EXPORTS = ("dsp_extract_lds_bytes", "dsp_extract_features", "dsp_extract_general_workspace_bytes",
            "dsp_extract_general", "dsp_knn_workspace_bytes", "dsp_knn_workspace_fallbacks_offset",
@@ -76,7 +77,9 @@ def load_library(path=LIB_PATH):
     L.dsp_zscore_apply.argtypes = [vp, i64, i32, vp, vp, vp, vp]
     L.dsp_abi_version.restype = i32
     L.dsp_abi_version.argtypes = []
-    if L.dsp_abi_version() != ABI_VERSION:
+    # DSP_ABI_ANY=1: A/B tools loading an older variant library (tools/ab_bench.sh); the queue
+    # scratch this binding passes (64 zero bytes) serves ABI 2's 8-byte counter pair too
+    if L.dsp_abi_version() != ABI_VERSION and not (os.environ.get("DSP_ABI_ANY") == "1" and L.dsp_abi_version() >= 2):
         raise HipError("%s has ABI %d, this binding expects %d: rebuild it" % (path, L.dsp_abi_version(), ABI_VERSION))
     _lib = L
     return L

@@ -143,7 +143,7 @@ class FeatureExtractor:
         if not wide and B > 0 and cap > 0:
             # the launch's own zeroed clip-queue counter pair: a capture of this call in a graph
             # gets its own from the graph's pool, so concurrent launches never share one
-            queue = torch.zeros(2, dtype=torch.int32, device=d)
+            queue = torch.zeros(_hip.QUEUE_WS_BYTES // 4, dtype=torch.int32, device=d)
             rc = _hip.lib().dsp_extract_features(
                 _hip.ptr(pcm), _hip.ptr(off), B, min(max_len, cap), self.L, self.S,
                 _hip.ptr(self.window), *args, _hip.ptr(queue), _hip.stream_handle(d))

@@ -30,7 +30,8 @@
 extern "C" {
 #endif
 
-#define DSP_ABI_VERSION 2  /* 2: dsp_extract_features takes the clip-queue scratch (queue_ws) */
+#define DSP_ABI_VERSION 3  /* 2: dsp_extract_features takes the clip-queue scratch (queue_ws);
+                              3: queue_ws is 64 bytes (per-XCD chunk counters) */
 
 /* return codes */
 #define DSP_OK 0
@@ -38,6 +39,8 @@ extern "C" {
 #define DSP_ERR_TOO_LONG 2    /* a clip does not fit the on-chip (LDS) pipeline */
 #define DSP_ERR_WORKSPACE 3   /* workspace too small */
 #define DSP_ERR_HIP 1000      /* + hipError_t of the failed launch */
+
+#define DSP_QUEUE_WS_BYTES 64  /* dsp_extract_features' queue_ws */
 
 /* per-clip status[b] (low byte) -- same codes as the oracle */
 #define DSP_CLIP_OK 0
@@ -90,11 +93,12 @@ size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int frame_shift)
  * seq       (optional, may be NULL): float32 [B, ld_seq, 3] per-frame (E, M, ZCR) -- the
  *           'sequence' method of extract_features_from_frames (:114-129); frames beyond
  *           ld_seq are dropped.
- * queue_ws  (optional, may be NULL): 8 bytes of device scratch, zero before the launch, the
- *           counter pair of the dynamic clip queue (persistent workgroups claim the next clip
- *           from it, so fast workgroups take more clips); the launch leaves it zero again, so it
- *           can be reused by the next launch on the same stream.  NULL: a static round-robin
- *           split of the clips over the workgroups (same results, ~6% slower at 100k clips).
+ * queue_ws  (optional, may be NULL): DSP_QUEUE_WS_BYTES (64) bytes of device scratch, zero
+ *           before the launch: the counters of the dynamic clip queue (persistent workgroups
+ *           claim chunks of consecutive clips, from their own XCD's share first, so fast
+ *           workgroups take more clips); the launch leaves it zero again, so it can be reused by
+ *           the next launch on the same stream.  NULL: a static round-robin split of the clips
+ *           over the workgroups (same results, slower).
  *           One launch at a time per queue_ws (see Conventions).
  */
 int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, int B, int64_t max_len,
