@@ -43,7 +43,10 @@
 #define DSP_ABL 0 // 1 = R4 frames, 2 = R5 jobs, 4 = R2 sign bits, 8 = VAD pass-A partial moments
 #endif
 #ifndef EXTRACT_R4_KV
-#define EXTRACT_R4_KV 9
+#define EXTRACT_R4_KV 8   // vectors per lane per unrolled R4 step (a multiple of EXTRACT_R4_PF)
+#endif
+#ifndef EXTRACT_R4_PF
+#define EXTRACT_R4_PF 4   // R4 crop loads in flight per lane
 #endif
 
 namespace dsp {
@@ -725,25 +728,26 @@ __device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur
 }
 
 // R4: windowed frames over the crop [st, en) (:378, :299-333; fe.py:12-43) -> c.fE / fM / fZ.
-// One 16-lane row per frame (4 frames per wave), in the canonical order of dsp_device.h: the
-// frame's clip-relative 8-sample vectors are re-read from L2 (16-B loads at the clip's own 2-byte
-// alignment) and lane rl takes vectors va + rl + 16k, so the sums do not depend on where the clip
-// sits in the buffer and equal dsp_extract_general's.  Per sample y = w_j x (the reference's
-// windowed frame, :329-331), E += y^2, M += |y|; the weights of a vector's 8 samples are two
-// aligned 16-B reads from the window copy shifted by fs mod 4.  Frame group g of 4 frames goes to
-// the wave whose rank (wrank, 0 .. NWAVE-1) is g mod NWAVE.  between() runs after the wave's first
-// batch of crop loads is issued and before it is used (other work hides the L2 latency).  Returns F.
-struct Nothing {
-    __device__ void operator()() const {}
-};
-template <typename Between = Nothing>
+// A 16-lane row takes a RUN of EXTRACT_R4_RUN consecutive frames; its lanes walk the run's
+// clip-relative 8-sample vectors in the canonical clip-absolute order of dsp_device.h (lane rl:
+// the vectors v = rl mod 16, re-read from L2 by 16-B loads at the clip's own 2-byte alignment),
+// so each vector is loaded and turned into (x^2, |x|) once for every frame of the run that holds
+// it, and the sums equal dsp_extract_general's (position independent).  Per frame and sample pair
+// e = fma(w^2, x^2, e), m = fma(w, |x|, m); the 8 (w, w^2) pairs of a vector are four aligned 16-B
+// reads from the window table copy of the right parity.  Runs go four to a wave (one per row),
+// run group g to the wave of rank (wrank) g mod NWAVE.  Returns F.
+#ifndef EXTRACT_R4_RUN
+#define EXTRACT_R4_RUN 2
+#endif
 __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int st, int en,
-                                         const ClipStats &cs, int j0, int j1, int wrank, int lane,
-                                         Between between = Nothing())
+                                         const ClipStats &cs, int j0, int j1, int wrank, int lane)
 {
+    constexpr int RUN = EXTRACT_R4_RUN;
+    constexpr int KV = EXTRACT_R4_KV;  // vectors per lane in one batch
     const int L = p.L, S = p.S, n = cur.n, lead = cur.lead;
     const int m = en - st;  // > 0 always (start < end)
     const int F = (m <= L) ? 1 : (m - L + S - 1) / S + 1;
+    const int nrun = (F + RUN - 1) / RUN;
     const float sE = cs.invMf * cs.invMf, sM = cs.invMf;
     const int wrow = EXTRACT_WROW(L);
     const CanonX cx = canon_x(cs.mq, cs.t0);
@@ -752,87 +756,100 @@ __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, c
     // vector boundary that dword holds the last sample, patched in from the aligned vector
     const int vfix = ((lead & 1) && ((lead + n) & 7) == 0) ? (n - 1) >> 3 : -1;
     const short klast = vfix >= 0 ? load_vec(p, cur, cur.nvec - 1)[7] : (short)0;
-    auto frame_vec = [&](auto padded_t, auto near_t, const short8 &x8, const float *wr, int jb, int lim,
-                         float2v &ea, float &m0, float &m1) {
-        constexpr bool PADDED = decltype(padded_t)::value, NEAR0 = decltype(near_t)::value;
-        const float4 wa = *reinterpret_cast<const float4 *>(wr + jb);
-        const float4 wb = *reinterpret_cast<const float4 *>(wr + jb + 4);
-        const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
-#pragma unroll
-        for (int h = 0; h < 4; h++) {
-            float2v w = {wv[2 * h], wv[2 * h + 1]};
-            if (PADDED) {  // samples past the crop are zero padding
-                const int j = jb + 2 * h;  // window index of the pair's first sample
-                w.x = j < lim ? w.x : 0.f;
-                w.y = j + 1 < lim ? w.y : 0.f;
-            }
-            canon_pair(w, canon_x2<NEAR0>(x8[2 * h], x8[2 * h + 1], cx), ea, m0, m1);
-        }
-    };
-    constexpr int R4_KV = EXTRACT_R4_KV;  // vectors per lane in one batch
     const int rl = lane & 15, row = lane >> 4;
-    auto frame_start = [&](int gi) {  // (sample coords) of this lane's row frame in group gi
-        const int g = 4 * gi + row;
-        return st + (g < F ? g : F - 1) * S;
+    // the run of this lane's row in run group gi: frames g0 .. g0 + RUN - 1 (those < F), vectors
+    // [va, vb]; the lane's first vector v0 (= rl mod 16)
+    auto run_geom = [&](int gi, int &g0, int &va, int &vb, int &v0) {
+        const int run = 4 * gi + row;
+        g0 = RUN * (run < nrun ? run : nrun - 1);
+        const int gl = min(g0 + RUN, F) - 1;
+        const int fs0 = st + g0 * S, fsl = st + gl * S;
+        va = fs0 >> 3;
+        vb = (fsl + min(L, en - fsl) - 1) >> 3;
+        v0 = canon_first(va, rl);
     };
-    // the first batch of the wave's first group, issued before between()
-    short8 xv[R4_KV];
-    const bool any = !(DSP_ABL & 1) && 4 * wrank < F;
-    if (any) {
-        const int va = frame_start(wrank) >> 3;
+    for (int gi = wrank; !(DSP_ABL & 1) && 4 * gi < nrun; gi += NWAVE) {
+        const bool act = 4 * gi + row < nrun;
+        int g0, va, vb, v0;
+        run_geom(gi, g0, va, vb, v0);
+        int fs[RUN], lim[RUN];
+        bool padded[RUN], in[RUN];
 #pragma unroll
-        for (int k = 0; k < R4_KV; k++) xv[k] = load_cvec(p, cur, va + rl + 16 * k);
-    }
-    between();
-    bool first = true;
-    for (int gi = wrank; any && 4 * gi < F; gi += NWAVE) {
-        const int g = 4 * gi + row;
-        const bool act = g < F;
-        const int fs = frame_start(gi);
-        const int lim = min(L, en - fs);  // samples beyond the crop are zero padding
-        const bool padded = lim < L;
-        const int va = fs >> 3, vb = (fs + lim - 1) >> 3;
-        const int r = fs & 3;  // copy whose rows start at window index = -fs (mod 4)
-        const float *wr = c.wtab + r * wrow + EXTRACT_WPAD + r;  // wr[j] = w[j], j = -7 .. L + 7
-        float2v ea = {0.f, 0.f};
-        float m0 = 0.f, m1 = 0.f;
-        for (int v0 = va; v0 <= vb; v0 += 16 * R4_KV) {
-            if (!first)
+        for (int j = 0; j < RUN; j++) {
+            in[j] = g0 + j < F;
+            fs[j] = st + (g0 + j) * S;
+            lim[j] = in[j] ? min(L, en - fs[j]) : 0;
+            padded[j] = lim[j] < L;
+        }
+        float2v e[RUN], mm[RUN];
 #pragma unroll
-                for (int k = 0; k < R4_KV; k++) xv[k] = load_cvec(p, cur, v0 + rl + 16 * k);
-            first = false;
-            if (vfix >= 0)  // clip-uniform, rare
+        for (int j = 0; j < RUN; j++) e[j] = mm[j] = (float2v){0.f, 0.f};
+        // a rolling window of R4_PF vectors in flight per lane: vector v + 16 R4_PF is requested
+        // as v is consumed (past vb the load is out of the descriptor's range: zeros, no traffic)
+        constexpr int PF = EXTRACT_R4_PF;
+        short8 xv[PF];
+        auto fetch = [&](int v) {
+            return __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  clip_rsrc(p, cur), v <= vb ? 2 * lead + 16 * v : 0x40000000, 0, 0));
+        };
 #pragma unroll
-                for (int k = 0; k < R4_KV; k++)
-                    if (v0 + rl + 16 * k == vfix) xv[k][(n - 1) & 7] = klast;
-            auto run = [&](auto pt, auto nt) {
+        for (int k = 0; k < PF; k++) xv[k] = fetch(v0 + 16 * k);
+        for (int vb0 = v0; vb0 <= vb; vb0 += 16 * KV) {
 #pragma unroll
-                for (int k = 0; k < R4_KV; k++) {
-                    const int v = v0 + rl + 16 * k;
-                    if (v <= vb) frame_vec(pt, nt, xv[k], wr, 8 * v - fs, lim, ea, m0, m1);
+            for (int k = 0; k < KV; k++) {
+                const int v = vb0 + 16 * k;
+                short8 x8 = xv[k % PF];
+                xv[k % PF] = fetch(v + 16 * PF);
+                if (v > vb) continue;
+                if (v == vfix) x8[(n - 1) & 7] = klast;  // vfix: clip-uniform, rare
+                float2v q[4], a[4];
+#pragma unroll
+                for (int h = 0; h < 4; h++) {
+                    const float2v x = cx.near0 ? canon_x2<true>(x8[2 * h], x8[2 * h + 1], cx)
+                                               : canon_x2<false>(x8[2 * h], x8[2 * h + 1], cx);
+                    canon_qa(x, q[h], a[h]);
                 }
-            };
-            if (padded)
-                cx.near0 ? run(BoolT<true>(), BoolT<true>()) : run(BoolT<true>(), BoolT<false>());
-            else if (cx.near0)
-                run(BoolT<false>(), BoolT<true>());
-            else
-                run(BoolT<false>(), BoolT<false>());
+#pragma unroll
+                for (int j = 0; j < RUN; j++) {
+                    const int jb = 8 * v - fs[j];  // window index of the vector's first sample
+                    if (!in[j] || jb <= -8 || jb >= lim[j]) continue;
+                    // copy r = jb & 1 holds (w, w^2)[i] at element i + WPAD + r: 16-B aligned here
+                    const int r = jb & 1;
+                    const float4 *wp = reinterpret_cast<const float4 *>(c.wtab + 2 * (r * wrow + jb + EXTRACT_WPAD + r));
+#pragma unroll
+                    for (int h = 0; h < 4; h++) {
+                        const float4 ww = wp[h];  // (w, w^2) of samples 2h, 2h + 1
+                        float2v w = {ww.x, ww.z}, w2 = {ww.y, ww.w};
+                        if (padded[j]) {  // samples past the crop are zero padding
+                            const int jj = jb + 2 * h;
+                            if (jj >= lim[j]) w.x = w2.x = 0.f;
+                            if (jj + 1 >= lim[j]) w.y = w2.y = 0.f;
+                        }
+                        canon_acc(w, w2, q[h], a[h], e[j], mm[j]);
+                    }
+                }
+                // one vector at a time: the scheduler would otherwise hoist every vector's window
+                // reads of the batch and run out of registers
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
-        const float E1 = dpp_row_reduce(ea.x + ea.y, OpAdd()) * sE;
-        const float M1 = dpp_row_reduce(m0 + m1, OpAdd()) * sM;
-        // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in
-        // [j0, j1]) and j < lim; transitions into the window's zero ends / padding count too
-        const int ia = fs + j0, ib = min(fs + j1, en - 1);  // sample coords
-        int z = dpp_row_reduce(ia < ib ? chg_count(c.posw, ia + lead, ib + lead, rl, 16) : 0, OpAdd());
-        if (ia <= ib) {
-            if (j0 > 0) z += pos_bit(c.posw, ia + lead);
-            if (ib < fs + L - 1) z += pos_bit(c.posw, ib + lead);
-        }
-        if (act && rl == 0) {
-            c.fE[g] = E1;
-            c.fM[g] = M1;
-            c.fZ[g] = z;
+#pragma unroll
+        for (int j = 0; j < RUN; j++) {
+            const float E1 = dpp_row_reduce(e[j].x + e[j].y, OpAdd()) * sE;
+            const float M1 = dpp_row_reduce(mm[j].x + mm[j].y, OpAdd()) * sM;
+            // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in
+            // [j0, j1]) and j < lim; transitions into the window's zero ends / padding count too
+            const int ia = fs[j] + j0, ib = min(fs[j] + j1, en - 1);  // sample coords
+            int z = dpp_row_reduce((in[j] && ia < ib) ? chg_count(c.posw, ia + lead, ib + lead, rl, 16) : 0, OpAdd());
+            if (ia <= ib) {
+                if (j0 > 0) z += pos_bit(c.posw, ia + lead);
+                if (ib < fs[j] + L - 1) z += pos_bit(c.posw, ib + lead);
+            }
+            if (act && in[j] && rl == 0) {
+                c.fE[g0 + j] = E1;
+                c.fM[g0 + j] = M1;
+                c.fZ[g0 + j] = z;
+            }
         }
     }
     return F;
@@ -1231,7 +1248,7 @@ __device__ __forceinline__ Ctx make_ctx(const ExtractParams &p, unsigned char *l
 // with a barrier.
 __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &c, int tid, int lane, int wid)
 {
-    float *wt = const_cast<float *>(c.wtab);
+    float *wt = const_cast<float *>(c.wtab);  // 2 copies of wrow (w, w^2) pairs
     Shared *sh = c.sh;
     const int L = p.L;
     constexpr int WPRE = 3;
@@ -1246,17 +1263,19 @@ __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &
         sh->j1 = -1;
     }
     const int wrow = EXTRACT_WROW(L);
-    for (int t = tid; t < 4 * (wrow - L); t += NT) {  // zero pads: m < WPAD + r, m >= L + WPAD + r
+    for (int t = tid; t < 2 * (wrow - L); t += NT) {  // zero pads: m < WPAD + r, m >= L + WPAD + r
         const int r = t / (wrow - L), q = t - r * (wrow - L);
-        wt[r * wrow + (q < EXTRACT_WPAD + r ? q : q + L)] = 0.f;
+        reinterpret_cast<float2v *>(wt)[r * wrow + (q < EXTRACT_WPAD + r ? q : q + L)] = (float2v){0.f, 0.f};
     }
     __syncthreads();
     auto put_weight = [&](int q0, double w) {  // weight j = q0 + lane (q0 wave-uniform)
         const int j = q0 + lane;
         const bool in = j < L;
         if (in) {
+            const float wf = (float)w;
+            const float2v e = {wf, canon_w2(wf)};
 #pragma unroll
-            for (int r = 0; r < 4; r++) wt[r * wrow + j + EXTRACT_WPAD + r] = (float)w;
+            for (int r = 0; r < 2; r++) reinterpret_cast<float2v *>(wt)[r * wrow + j + EXTRACT_WPAD + r] = e;
         }
         const unsigned long long m = __ballot(in && w > 0.0);
         if (lane == 0 && m) {
@@ -1525,15 +1544,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
         __syncthreads();  // B2
 
         // ---- S3 --------------------------------------------------------------------------------
-        // A's first crop loads go out first; B's VAD frames (LDS work) run under their latency
-        auto vadB = [&]() {
-            if (okB && sb.nv > 0) vad_frames_fast(cB, rb, L, S, sb, qa, pa_w, pa_e0, pa_e1, tid);
-        };
+        // B's VAD frames (one lane pair per frame: waves 0-3) and A's crop frames (runs of two
+        // frames, four per wave: waves 7, 6, 5, 4 first) mostly run on different waves
+        if (okB && sb.nv > 0) vad_frames_fast(cB, rb, L, S, sb, qa, pa_w, pa_e0, pa_e1, tid);
         int F = 0;
-        if (actA)
-            F = r4_frames(p, cA, ra, st, en, sa, j0, j1, NWAVE - 1 - wid, lane, vadB);  // waves 7, 6, .. first
-        else
-            vadB();
+        if (actA) F = r4_frames(p, cA, ra, st, en, sa, j0, j1, NWAVE - 1 - wid, lane);
         STAMPW(ib, 12, NWAVE - 1);
         STAMPW(ib, 14, 0);
         __syncthreads();  // B3

@@ -20,8 +20,9 @@
 #define EXTRACT_LDS_LIMIT (160 * 1024)   // one CU
 #define EXTRACT_SHARED_BYTES 512         // sizeof(dsp::Shared) rounded up (static_assert'ed)
 #define EXTRACT_WPAD 8                   // zero window entries on each side of the window table
-// floats per shifted window copy: copy r holds w[m - WPAD - r] at m (zero outside [0, L)), so
-// that 4 consecutive weights starting at any window index are one aligned 16-B LDS read
+// (w, w^2) pairs per shifted window copy: copy r (0, 1) holds them for window index m - WPAD - r at
+// element m (zero outside [0, L)), so that the 8 pairs of a vector starting at any window index
+// are four aligned 16-B LDS reads from the copy of that index's parity
 #define EXTRACT_WROW(L) ((((L) + 2 * EXTRACT_WPAD + 4) + 3) & ~3)
 
 struct ExtractCarve {
@@ -46,7 +47,7 @@ __host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvc
     c.fcap = fcap;
     c.nwmax = nwmax;
     DSP_TAKE(sh, EXTRACT_SHARED_BYTES);
-    DSP_TAKE(wtab, 16 * wrow);                   // 4 zero-padded copies of w, shifted by 0..3
+    DSP_TAKE(wtab, 16 * wrow);                   // 2 zero-padded copies of (w, w^2), shifted by 0..1
     DSP_TAKE(posw, 4 * (c.nwmax + 2));           // positive-sample bits (+2 zero sentinels)
     DSP_TAKE(wS2, 8 * c.nwmax);                  // per word: sum k^2 (exact, u64)
     DSP_TAKE(wS1, 4 * c.nwmax);                  // per word: sum k

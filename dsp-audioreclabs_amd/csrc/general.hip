@@ -395,19 +395,19 @@ __device__ __forceinline__ void general_clip(const Params &p, Sh &s, const Ws &w
         const int64_t fs = st + (act ? g : F - 1) * S;
         const int64_t lim = min((int64_t)L, en - fs);
         const int64_t va = fs >> 3, vb = (fs + lim - 1) >> 3;
-        float2v ea = {0.f, 0.f};
-        float m0 = 0.f, m1 = 0.f;
-        for (int64_t v = va + rl; v <= vb; v += 16)
+        float2v ea = {0.f, 0.f}, ma = {0.f, 0.f};
+        for (int64_t v = va + ((rl - va) & 15); v <= vb; v += 16)  // clip-absolute: v = rl (mod 16)
             for (int h = 0; h < 4; h++) {
-                float2v wv, xv;
+                float2v wv, xv, q, a;
                 for (int t = 0; t < 2; t++) {
                     const int64_t sj = 8 * v + 2 * h + t, j = sj - fs;
                     wv[t] = (j >= 0 && j < lim) ? (float)p.window[j] : 0.f;
                     xv[t] = sj < n ? canon_xval(sample(x, sj), cx) : 0.f;
                 }
-                canon_pair(wv, xv, ea, m0, m1);
+                canon_qa(xv, q, a);
+                canon_acc(wv, canon_w2(wv), q, a, ea, ma);
             }
-        const float es = dpp_row_reduce(ea.x + ea.y, OpAdd()), ms = dpp_row_reduce(m0 + m1, OpAdd());
+        const float es = dpp_row_reduce(ea.x + ea.y, OpAdd()), ms = dpp_row_reduce(ma.x + ma.y, OpAdd());
         int zc = 0;
         for (int j = rl; j + 1 < L; j += 16) {
             const bool p0 = j < lim && p.window[j] > 0.0 && sample(x, fs + j) >= tpos;

@@ -11,7 +11,7 @@ if [ $TESTS = 1 ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
   tail -2 $O/gpu_tests.log
 fi
-bash tools/ab_bench.sh 100000 r03 pipe0 base > $O/ab100k.txt 2>&1; cat $O/ab100k.txt
+bash tools/ab_bench.sh 100000 r03 pipe1 base > $O/ab100k.txt 2>&1; cat $O/ab100k.txt
 for nq in 12500 100000; do
   timeout -k 10 200 python3 tools/bench_knn.py --no-cpu --queries $nq > $O/knn_$nq.json; cat $O/knn_$nq.json
 done
