@@ -43,10 +43,10 @@
 #define DSP_ABL 0 // 1 = R4 frames, 2 = R5 jobs, 4 = R2 sign bits, 8 = VAD pass-A partial moments
 #endif
 #ifndef EXTRACT_R4_KV
-#define EXTRACT_R4_KV 8   // vectors per lane per unrolled R4 step (a multiple of EXTRACT_R4_PF)
+#define EXTRACT_R4_KV 10  // vectors per lane per unrolled R4 step (a multiple of EXTRACT_R4_PF)
 #endif
 #ifndef EXTRACT_R4_PF
-#define EXTRACT_R4_PF 4   // R4 crop loads in flight per lane
+#define EXTRACT_R4_PF 5   // R4 crop loads in flight per lane (the most at 128 VGPRs without spills)
 #endif
 
 namespace dsp {
@@ -132,6 +132,7 @@ struct Shared {
     double noise_e, noise_z;  // VAD noise estimates (:189-195, :239-245)
     double oslo[3], oshi[3];  // order statistics (F-1)/2 and F/2 of E, M, ZCR (medians)
     int n3, n1, n6, exact, j0, j1, next;
+    int qnext, qend, qcursor;  // clip queue (thread 0): the current chunk's next clip and end; static split
 };
 static_assert(sizeof(Shared) <= EXTRACT_SHARED_BYTES, "grow EXTRACT_SHARED_BYTES");
 
@@ -1301,31 +1302,36 @@ __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &
 #ifndef EXTRACT_CHUNK
 #define EXTRACT_CHUNK 4
 #endif
-struct ClipQueue {
+struct ClipQueue {  // wave-uniform; the mutable state lives in Shared (thread 0 only)
     unsigned *q;
     int B, nch, xcd;
-    int next, end;  // the current chunk's next clip and its end
-    int cursor;     // static split
 };
-__device__ __forceinline__ ClipQueue queue_open(const ExtractParams &p)
+__device__ __forceinline__ ClipQueue queue_open(const ExtractParams &p, Shared *sh)
 {
     ClipQueue Q;
     Q.q = p.queue;
     Q.B = p.B;
     Q.nch = (p.B + EXTRACT_CHUNK - 1) / EXTRACT_CHUNK;
     Q.xcd = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;  // HW_REG_XCC_ID[3:0]
-    Q.next = Q.end = 0;
-    Q.cursor = (int)blockIdx.x - (int)gridDim.x;
+    if (threadIdx.x == 0) {
+        sh->qnext = sh->qend = 0;
+        sh->qcursor = (int)blockIdx.x - (int)gridDim.x;
+    }
     return Q;
 }
-// the next clip of this workgroup, -1 when none is left
-__device__ __forceinline__ int queue_next(ClipQueue &Q)
+// the next clip of this workgroup, -1 when none is left.  Thread 0 only.
+__device__ __forceinline__ int queue_next(const ClipQueue &Q, Shared *sh)
 {
     if (!Q.q) {
-        Q.cursor += gridDim.x;
-        return Q.cursor < Q.B ? Q.cursor : -1;
+        const int c = sh->qcursor + (int)gridDim.x;
+        sh->qcursor = c;
+        return c < Q.B ? c : -1;
     }
-    if (Q.next < Q.end) return Q.next++;
+    const int nx = sh->qnext;
+    if (nx < sh->qend) {
+        sh->qnext = nx + 1;
+        return nx;
+    }
     for (int t = 0; t < 8; t++) {
         const int y = (Q.xcd + t) & 7;
         const unsigned c0 = (unsigned)(y * Q.nch / 8), c1 = (unsigned)((y + 1) * Q.nch / 8);
@@ -1333,9 +1339,10 @@ __device__ __forceinline__ int queue_next(ClipQueue &Q)
         if (c0 + __hip_atomic_load(Q.q + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= c1) continue;
         const unsigned c = c0 + __hip_atomic_fetch_add(Q.q + y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (c < c1) {
-            Q.next = (int)c * EXTRACT_CHUNK;
-            Q.end = min(Q.B, Q.next + EXTRACT_CHUNK);
-            return Q.next++;
+            const int first = (int)c * EXTRACT_CHUNK;
+            sh->qnext = first + 1;
+            sh->qend = min(Q.B, first + EXTRACT_CHUNK);
+            return first;
         }
     }
     return -1;
@@ -1369,8 +1376,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     WG_STAMP(16);
     build_window(p, c, tid, lane, wid);
-    ClipQueue Q = queue_open(p);
-    if (tid == 0) sh->next = queue_next(Q);
+    const ClipQueue Q = queue_open(p, sh);
+    if (tid == 0) sh->next = queue_next(Q, sh);
     __syncthreads();
     short8 regs[NRV];
     bool inflight = false;  // regs already hold clip i's loads (issued by the previous clip's R4)
@@ -1379,12 +1386,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
         int claim = -1;
         if (!cur.ok) {
             __syncthreads();  // everyone has read sh->next (the ok path has barriers in clip_body)
-            if (tid == 0) claim = queue_next(Q);
+            if (tid == 0) claim = queue_next(Q, sh);
             write_bad_clip(p, i, tid);
             inflight = false;
         } else {
             if (!inflight) issue_clip(regs, p, cur);
-            if (tid == 0) claim = queue_next(Q);
+            if (tid == 0) claim = queue_next(Q, sh);
             c.stamp_clip = i;
             const bool done = clip_body<false, false>(p, c, i, cur, regs, claim);
             if (!done && tid == 0) p.status[i] = DSP_CLIP_UNCERTIFIED;
@@ -1439,8 +1446,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     build_window(p, c0, (int)threadIdx.x, (int)threadIdx.x & 63, wid);
     const int j0 = uni(shs0->j0), j1 = uni(shs0->j1);
 
-    ClipQueue Q = queue_open(p);
-    if (threadIdx.x == 0) shs0->next = queue_next(Q);
+    const ClipQueue Q = queue_open(p, shs0);
+    if (threadIdx.x == 0) shs0->next = queue_next(Q, shs0);
     __syncthreads();
     int inext = uni(shs0->next);  // the clip whose words are in flight
     ClipRef rnext = inext >= 0 ? clip_ref(p, inext) : clip_none();
@@ -1480,7 +1487,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
         STAMPW(ib, 0, 0);
 
         // ---- S1 --------------------------------------------------------------------------------
-        if (tid == 0) shs0->next = ib >= 0 ? queue_next(Q) : -1;
+        if (tid == 0) shs0->next = ib >= 0 ? queue_next(Q, shs0) : -1;
         if (wid == 0 && okA && sa.nv > 0) {
             // the scan is the trip's single-wave critical path: issue priority over the
             // co-resident workgroup's waves
