@@ -67,8 +67,9 @@ def load_library(path=LIB_PATH):
                                       vp, vp, vp, vp, vp, vp, i32, vp, i32, vp, sz, vp]
     L.dsp_knn_workspace_bytes.restype = sz
     L.dsp_knn_workspace_bytes.argtypes = [i64, i64, i32, i32]
-    L.dsp_knn_workspace_fallbacks_offset.restype = sz
-    L.dsp_knn_workspace_fallbacks_offset.argtypes = [i64, i64, i32, i32]
+    if hasattr(L, "dsp_knn_workspace_fallbacks_offset") or os.environ.get("DSP_ABI_ANY") != "1":
+        L.dsp_knn_workspace_fallbacks_offset.restype = sz  # (older A/B variants lack it)
+        L.dsp_knn_workspace_fallbacks_offset.argtypes = [i64, i64, i32, i32]
     L.dsp_knn_classify.restype = i32
     L.dsp_knn_classify.argtypes = [vp, vp, i64, vp, i64, i32, i32, i64, i32, vp, vp, vp, vp, sz, vp]
     L.dsp_zscore_fit.restype = i32
