@@ -10,7 +10,7 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD S
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_VMEM" \
            "SQC_ICACHE_MISSES SQC_ICACHE_HITS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_FLAT SQ_INSTS_VMEM_WR"; do
   i=$((i+1))
-  DSP_LIB_PATH=$lib timeout -s KILL 90 rocprofv3 --pmc $set --output-format csv -d $O/p$i -o p -- python3 $R/bench.py --no-cpu --knn-ref 0 --sweep-clips 0 --steps 2 --warmup 1 --no-graph --clips $C > $O/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $O/p$i.log; }
+  DSP_LIB_PATH=$lib timeout -s KILL 90 rocprofv3 --pmc $set --output-format csv -d $O/p$i -o p -- python3 $R/bench.py --no-cpu --knn-ref 0 --sweep-clips 0 --no-cfg0 --small-clips 0 --steps 2 --warmup 1 --no-graph --clips $C > $O/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $O/p$i.log; }
 done
 python3 - $O > $O/pmc_summary.txt <<'PY'
 import csv, glob, sys, collections
