@@ -43,10 +43,10 @@
 #define DSP_ABL 0 // 1 = R4 frames, 2 = R5 jobs, 4 = R2 sign bits, 8 = VAD pass-A partial moments
 #endif
 #ifndef EXTRACT_R4_KV
-#define EXTRACT_R4_KV 10  // vectors per lane per unrolled R4 step (a multiple of EXTRACT_R4_PF)
+#define EXTRACT_R4_KV 9   // vectors per lane per unrolled R4 step (a multiple of EXTRACT_R4_PF)
 #endif
 #ifndef EXTRACT_R4_PF
-#define EXTRACT_R4_PF 5   // R4 crop loads in flight per lane (the most at 128 VGPRs without spills)
+#define EXTRACT_R4_PF 9   // R4 crop loads in flight per lane: a whole 1102-sample frame (RUN 1)
 #endif
 
 namespace dsp {
@@ -208,10 +208,20 @@ __device__ __forceinline__ void issue_word(short8 *q, const ExtractParams &p, co
 }
 
 // the clip's first RREG words into registers (word r * NT + tid -> regs[4r .. 4r+3])
-__device__ __forceinline__ void issue_clip(short8 (&regs)[NRV], const ExtractParams &p, const ClipRef &c)
+__device__ __forceinline__ void issue_clip(short8 (&regs)[NRV], const ExtractParams &p, const ClipRef &c,
+                                           int tid = (int)threadIdx.x)
 {
 #pragma unroll
-    for (int r = 0; r < RREG; r++) issue_word(&regs[4 * r], p, c, r * NT + (int)threadIdx.x);
+    for (int r = 0; r < RREG; r++) issue_word(&regs[4 * r], p, c, r * NT + tid);
+}
+// the thread index, opaque to the optimiser where it is taken (once per clip): index arithmetic
+// that depends only on it (word numbers, lane masks of the sorts) is then recomputed per clip
+// instead of being hoisted out of the persistent loop and kept live (spilled) across it
+__device__ __forceinline__ int opaque_tid()
+{
+    int t = (int)threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
 }
 
 // VAD noise estimates (src/audio_processing.py:188-195, :239-245) by one wave into sh->noise_e /
@@ -738,7 +748,7 @@ __device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur
 // reads from the window table copy of the right parity.  Runs go four to a wave (one per row),
 // run group g to the wave of rank (wrank) g mod NWAVE.  Returns F.
 #ifndef EXTRACT_R4_RUN
-#define EXTRACT_R4_RUN 2
+#define EXTRACT_R4_RUN 1
 #endif
 __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int st, int en,
                                          const ClipStats &cs, int j0, int j1, int wrank, int lane)
@@ -915,7 +925,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
                                           short8 (&regs)[NRV], int claim = -1)
 {
     Shared *sh = c.sh;
-    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
+    const int tid = opaque_tid(), lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
     const int L = p.L, S = p.S;
     const int n = cur.n, lead = cur.lead, nword = cur.nword;
     float *featb = p.feat + (size_t)i * 15;
@@ -1127,7 +1137,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
         // regs are dead since R2: the next clip's words load while R5 runs (unconditional, a
         // clip_none() reads zeros, so the compiler's vmcnt bookkeeping stays exact)
         const int nx = sh->next;
-        issue_clip(regs, p, nx >= 0 ? clip_ref(p, nx) : clip_none());
+        issue_clip(regs, p, nx >= 0 ? clip_ref(p, nx) : clip_none(), tid);
     }
     STAMP(i, 5);
 
@@ -1360,18 +1370,31 @@ __device__ __forceinline__ void queue_done(const ExtractParams &p)
     }
 }
 
+// FAST launches: 0 = extract_kernel<true> (one clip at a time per workgroup), 1 = the two-clip
+// pipeline extract_pipe_kernel.  The pipeline overlaps the single-wave phases of one clip with the
+// multi-wave phases of the other, but the CU is bound by instruction issue (about one issuing wave
+// per SIMD per 4-cycle slot at 100 000 clips), and the pipeline adds 10% VALU and 49% SALU
+// instructions: 3.41 against 3.35 ms (profiles/r04d_*), so the one-clip loop ships.
+#ifndef EXTRACT_PIPE
+#define EXTRACT_PIPE 0
+#endif
+#if !EXTRACT_PIPE
+#define EXTRACT_PIPE_UNUSED __attribute__((unused))
+#endif
+
 // 128 VGPRs: two 512-thread workgroups per CU
 #ifndef EXTRACT_WAVES_PER_EU
 #define EXTRACT_WAVES_PER_EU 4
 #endif
 
-// ---- generic layout (clips past the FAST plan): one clip at a time per workgroup -------------
+// ---- one clip at a time per workgroup (both layouts) --------------------------------------------
 // A near tie (an endpoint decision within the certification margin) leaves the clip with status
 // DSP_CLIP_UNCERTIFIED; extract_exact_kernel, launched next on the stream, redoes it.
+template <bool FAST>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVES_PER_EU))) void extract_kernel(ExtractParams p)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    Ctx c = make_ctx<false>(p, lds);
+    Ctx c = make_ctx<FAST>(p, lds);
     Shared *sh = c.sh;
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     WG_STAMP(16);
@@ -1393,7 +1416,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
             if (!inflight) issue_clip(regs, p, cur);
             if (tid == 0) claim = queue_next(Q, sh);
             c.stamp_clip = i;
-            const bool done = clip_body<false, false>(p, c, i, cur, regs, claim);
+            const bool done = clip_body<false, FAST>(p, c, i, cur, regs, claim);
             if (!done && tid == 0) p.status[i] = DSP_CLIP_UNCERTIFIED;
             inflight = done;  // a deferred clip returns before R4
         }
@@ -1671,7 +1694,9 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
         g_num_cus[dev] = prop.multiProcessorCount;
         (void)hipFuncSetAttribute((const void *)dsp::extract_pipe_kernel,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
-        (void)hipFuncSetAttribute((const void *)dsp::extract_kernel,
+        (void)hipFuncSetAttribute((const void *)dsp::extract_kernel<true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
+        (void)hipFuncSetAttribute((const void *)dsp::extract_kernel<false>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
         (void)hipFuncSetAttribute((const void *)dsp::extract_exact_kernel<true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
@@ -1713,10 +1738,14 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     const int grid = B < slots ? B : slots;
     const hipStream_t s = (hipStream_t)stream;
     if (fast) {
+#if EXTRACT_PIPE
         hipLaunchKernelGGL(dsp::extract_pipe_kernel, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
+#else
+        hipLaunchKernelGGL(dsp::extract_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
+#endif
         hipLaunchKernelGGL(dsp::extract_exact_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
     } else {
-        hipLaunchKernelGGL(dsp::extract_kernel, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
+        hipLaunchKernelGGL(dsp::extract_kernel<false>, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
         hipLaunchKernelGGL(dsp::extract_exact_kernel<false>, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
     }
     const hipError_t e = hipGetLastError();

@@ -5,7 +5,7 @@ R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CS = os.path.join(R, "dsp-audioreclabs_amd", "csrc")
 asm = sys.argv[1] if len(sys.argv) > 1 else "/tmp/extract_g.s"
 if len(sys.argv) == 1:
-    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", "-I" + os.path.join(R, "include"),
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", "-I" + os.path.join(R, "include"), "-I" + CS,
                     "--offload-device-only", "-gline-tables-only", "-S", os.path.join(CS, "extract.hip"), "-o", asm], check=True)
 src = open(os.path.join(CS, "extract.hip")).read().split("\n")
 body = ([i + 1 for i, l in enumerate(src) if "bool clip_body(" in l][0],

@@ -2,6 +2,7 @@
 import collections, csv, glob, os, sys
 d = sys.argv[1]
 ks = sys.argv[2] if len(sys.argv) > 2 else "extract_kernel"
+split = len(sys.argv) > 3
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
     for r in csv.DictReader(open(f)):
