@@ -783,73 +783,75 @@ __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, c
         const bool act = 4 * gi + row < nrun;
         int g0, va, vb, v0;
         run_geom(gi, g0, va, vb, v0);
-        int fs[RUN], lim[RUN];
-        bool padded[RUN], in[RUN];
+        int fs[RUN];
+        bool in[RUN];
 #pragma unroll
         for (int j = 0; j < RUN; j++) {
             in[j] = g0 + j < F;
             fs[j] = st + (g0 + j) * S;
-            lim[j] = in[j] ? min(L, en - fs[j]) : 0;
-            padded[j] = lim[j] < L;
         }
         float2v e[RUN], mm[RUN];
 #pragma unroll
         for (int j = 0; j < RUN; j++) e[j] = mm[j] = (float2v){0.f, 0.f};
-        // a rolling window of R4_PF vectors in flight per lane: vector v + 16 R4_PF is requested
-        // as v is consumed (past vb the load is out of the descriptor's range: zeros, no traffic)
-        constexpr int PF = EXTRACT_R4_PF;
-        short8 xv[PF];
-        auto fetch = [&](int v) {
-            return __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(
-                                                  clip_rsrc(p, cur), v <= vb ? 2 * lead + 16 * v : 0x40000000, 0, 0));
-        };
-#pragma unroll
-        for (int k = 0; k < PF; k++) xv[k] = fetch(v0 + 16 * k);
+        // samples at or past the crop end en are the zero padding of frame_signal: their x is set
+        // to 0 (fma(w^2, 0, e) = e, the bits of a zero weight) -- only rows whose run reaches en
+        const bool padded = 8 * vb + 8 > en;
         for (int vb0 = v0; vb0 <= vb; vb0 += 16 * KV) {
+            short8 xv[KV];
 #pragma unroll
-            for (int k = 0; k < KV; k++) {
-                const int v = vb0 + 16 * k;
-                short8 x8 = xv[k % PF];
-                xv[k % PF] = fetch(v + 16 * PF);
-                if (v > vb) continue;
-                if (v == vfix) x8[(n - 1) & 7] = klast;  // vfix: clip-uniform, rare
-                float2v q[4], a[4];
+            for (int k = 0; k < KV; k++) xv[k] = load_cvec(p, cur, vb0 + 16 * k);
+            if (vfix >= 0)  // clip-uniform, rare
 #pragma unroll
-                for (int h = 0; h < 4; h++) {
-                    const float2v x = cx.near0 ? canon_x2<true>(x8[2 * h], x8[2 * h + 1], cx)
-                                               : canon_x2<false>(x8[2 * h], x8[2 * h + 1], cx);
-                    canon_qa(x, q[h], a[h]);
-                }
+                for (int k = 0; k < KV; k++)
+                    if (vb0 + 16 * k == vfix) xv[k][(n - 1) & 7] = klast;
+            auto run = [&](auto pad_t, auto near_t) {
+                constexpr bool PADDED = decltype(pad_t)::value, NEAR0 = decltype(near_t)::value;
 #pragma unroll
-                for (int j = 0; j < RUN; j++) {
-                    const int jb = 8 * v - fs[j];  // window index of the vector's first sample
-                    if (!in[j] || jb <= -8 || jb >= lim[j]) continue;
-                    // copy r = jb & 1 holds (w, w^2)[i] at element i + WPAD + r: 16-B aligned here
-                    const int r = jb & 1;
-                    const float4 *wp = reinterpret_cast<const float4 *>(c.wtab + 2 * (r * wrow + jb + EXTRACT_WPAD + r));
+                for (int k = 0; k < KV; k++) {
+                    const int v = vb0 + 16 * k;
+                    if (v > vb) continue;
+                    float2v q[4], a[4];
 #pragma unroll
                     for (int h = 0; h < 4; h++) {
-                        const float4 ww = wp[h];  // (w, w^2) of samples 2h, 2h + 1
-                        float2v w = {ww.x, ww.z}, w2 = {ww.y, ww.w};
-                        if (padded[j]) {  // samples past the crop are zero padding
-                            const int jj = jb + 2 * h;
-                            if (jj >= lim[j]) w.x = w2.x = 0.f;
-                            if (jj + 1 >= lim[j]) w.y = w2.y = 0.f;
+                        float2v x = canon_x2<NEAR0>(xv[k][2 * h], xv[k][2 * h + 1], cx);
+                        if (PADDED) {
+                            const int u = 8 * v + 2 * h;  // clip sample of the pair's first element
+                            x.x = u < en ? x.x : 0.f;
+                            x.y = u + 1 < en ? x.y : 0.f;
                         }
-                        canon_acc(w, w2, q[h], a[h], e[j], mm[j]);
+                        canon_qa(x, q[h], a[h]);
+                    }
+#pragma unroll
+                    for (int j = 0; j < RUN; j++) {
+                        const int jb = 8 * v - fs[j];  // window index of the vector's first sample
+                        if (RUN > 1 && (!in[j] || jb <= -8 || jb >= L)) continue;
+                        // copy r = jb & 1, pair slot (jb + WPAD + r) / 2: {w, w, w^2, w^2} of the
+                        // samples jb + 2h, jb + 2h + 1 at slot + h
+                        const int r = jb & 1;
+                        const float4 *wp = reinterpret_cast<const float4 *>(c.wtab) + r * (wrow / 2) +
+                                           ((jb + EXTRACT_WPAD + r) >> 1);
+#pragma unroll
+                        for (int h = 0; h < 4; h++) {
+                            const float4 ww = wp[h];
+                            canon_acc((float2v){ww.x, ww.y}, (float2v){ww.z, ww.w}, q[h], a[h], e[j], mm[j]);
+                        }
                     }
                 }
-                // one vector at a time: the scheduler would otherwise hoist every vector's window
-                // reads of the batch and run out of registers
-                __builtin_amdgcn_sched_barrier(0);
-            }
+            };
+            if (padded)
+                cx.near0 ? run(BoolT<true>(), BoolT<true>()) : run(BoolT<true>(), BoolT<false>());
+            else if (cx.near0)
+                run(BoolT<false>(), BoolT<true>());
+            else
+                run(BoolT<false>(), BoolT<false>());
         }
 #pragma unroll
         for (int j = 0; j < RUN; j++) {
             const float E1 = dpp_row_reduce(e[j].x + e[j].y, OpAdd()) * sE;
             const float M1 = dpp_row_reduce(mm[j].x + mm[j].y, OpAdd()) * sM;
             // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in
-            // [j0, j1]) and j < lim; transitions into the window's zero ends / padding count too
+            // [j0, j1]) and before the crop end; transitions into the window's zero ends /
+            // padding count too
             const int ia = fs[j] + j0, ib = min(fs[j] + j1, en - 1);  // sample coords
             int z = dpp_row_reduce((in[j] && ia < ib) ? chg_count(c.posw, ia + lead, ib + lead, rl, 16) : 0, OpAdd());
             if (ia <= ib) {
@@ -926,7 +928,10 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
 {
     Shared *sh = c.sh;
     const int tid = opaque_tid(), lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
-    const int L = p.L, S = p.S;
+    // frame sizes opaque per clip as well: constants derived from them ((double)L, ...) are
+    // recomputed in the clip instead of being kept live across the loop
+    int L = p.L, S = p.S;
+    asm volatile("" : "+s"(L), "+s"(S));
     const int n = cur.n, lead = cur.lead, nword = cur.nword;
     float *featb = p.feat + (size_t)i * 15;
     const int16_t *clip_g = p.pcm + cur.base + lead;  // the clip in global memory, sample coords
@@ -1274,19 +1279,23 @@ __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &
         sh->j1 = -1;
     }
     const int wrow = EXTRACT_WROW(L);
-    for (int t = tid; t < 2 * (wrow - L); t += NT) {  // zero pads: m < WPAD + r, m >= L + WPAD + r
-        const int r = t / (wrow - L), q = t - r * (wrow - L);
-        reinterpret_cast<float2v *>(wt)[r * wrow + (q < EXTRACT_WPAD + r ? q : q + L)] = (float2v){0.f, 0.f};
-    }
+    // copy r (0, 1), pair slot i = {w_a, w_a+1, w2_a, w2_a+1} of window indices a = 2i - WPAD - r
+    // (zero outside [0, L)): the 8 (w, w^2) of a vector starting at any window index are four
+    // aligned 16-B reads from the copy of that index's parity, already in register-pair order
+    for (int t = tid; t < 2 * wrow; t += NT) wt[(t / wrow) * 2 * wrow + 2 * (t % wrow) + 0] = 0.f;
+    for (int t = tid; t < 2 * wrow; t += NT) wt[(t / wrow) * 2 * wrow + 2 * (t % wrow) + 1] = 0.f;
     __syncthreads();
     auto put_weight = [&](int q0, double w) {  // weight j = q0 + lane (q0 wave-uniform)
         const int j = q0 + lane;
         const bool in = j < L;
         if (in) {
             const float wf = (float)w;
-            const float2v e = {wf, canon_w2(wf)};
 #pragma unroll
-            for (int r = 0; r < 2; r++) reinterpret_cast<float2v *>(wt)[r * wrow + j + EXTRACT_WPAD + r] = e;
+            for (int r = 0; r < 2; r++) {
+                const int m = j + EXTRACT_WPAD + r;  // slot m >> 1, position m & 1
+                wt[r * 2 * wrow + 4 * (m >> 1) + (m & 1)] = wf;
+                wt[r * 2 * wrow + 4 * (m >> 1) + 2 + (m & 1)] = canon_w2(wf);
+            }
         }
         const unsigned long long m = __ballot(in && w > 0.0);
         if (lane == 0 && m) {
