@@ -220,7 +220,9 @@ __device__ __forceinline__ void issue_clip(short8 (&regs)[NRV], const ExtractPar
 __device__ __forceinline__ int opaque_tid()
 {
     int t = (int)threadIdx.x;
+#ifndef EXTRACT_NO_OPAQUE_TID
     asm volatile("" : "+v"(t));
+#endif
     return t;
 }
 
@@ -931,7 +933,9 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     // frame sizes opaque per clip as well: constants derived from them ((double)L, ...) are
     // recomputed in the clip instead of being kept live across the loop
     int L = p.L, S = p.S;
+#ifndef EXTRACT_NO_OPAQUE_LS
     asm volatile("" : "+s"(L), "+s"(S));
+#endif
     const int n = cur.n, lead = cur.lead, nword = cur.nword;
     float *featb = p.feat + (size_t)i * 15;
     const int16_t *clip_g = p.pcm + cur.base + lead;  // the clip in global memory, sample coords
