@@ -1325,6 +1325,9 @@ __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &
 #ifndef EXTRACT_CHUNK
 #define EXTRACT_CHUNK 4
 #endif
+#ifndef EXTRACT_XCD_RANGES
+#define EXTRACT_XCD_RANGES 8  // 1: one range for every workgroup (A/B)
+#endif
 struct ClipQueue {  // wave-uniform; the mutable state lives in Shared (thread 0 only)
     unsigned *q;
     int B, nch, xcd;
@@ -1355,9 +1358,10 @@ __device__ __forceinline__ int queue_next(const ClipQueue &Q, Shared *sh)
         sh->qnext = nx + 1;
         return nx;
     }
-    for (int t = 0; t < 8; t++) {
-        const int y = (Q.xcd + t) & 7;
-        const unsigned c0 = (unsigned)(y * Q.nch / 8), c1 = (unsigned)((y + 1) * Q.nch / 8);
+    constexpr int NR = EXTRACT_XCD_RANGES;
+    for (int t = 0; t < NR; t++) {
+        const int y = (Q.xcd + t) % NR;
+        const unsigned c0 = (unsigned)(y * Q.nch / NR), c1 = (unsigned)((y + 1) * Q.nch / NR);
         // a relaxed look first: exhausted ranges cost no atomic
         if (c0 + __hip_atomic_load(Q.q + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= c1) continue;
         const unsigned c = c0 + __hip_atomic_fetch_add(Q.q + y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1643,20 +1647,33 @@ __global__ __launch_bounds__(NT) void extract_exact_kernel(ExtractParams p)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     Ctx c = make_ctx<FAST>(p, lds);
+    Shared *sh = c.sh;
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // NT ints past the layout (the host launches this kernel with 4 NT more bytes of LDS)
+    int *list = reinterpret_cast<int *>(lds + (FAST ? extract_carve_fast().total : p.cv.total));
     bool built = false;
-    for (int i = blockIdx.x; i < p.B; i += gridDim.x) {
-        if (__builtin_amdgcn_readfirstlane(p.status[i]) != DSP_CLIP_UNCERTIFIED) continue;
-        if (!built) {
-            build_window(p, c, tid, lane, wid);
-            built = true;
-        }
-        c.stamp_clip = i;
-        const ClipRef cr = clip_ref(p, i);
-        short8 regs[NRV];
-        issue_clip(regs, p, cr);
-        clip_body<true, FAST>(p, c, i, cr, regs);
+    // the workgroup's clips blockIdx.x + G (t + NT k), NT statuses read at once, the near ties listed
+    for (int64_t b0 = 0; b0 < p.B; b0 += (int64_t)gridDim.x * NT) {
+        const int64_t i = b0 + blockIdx.x + (int64_t)gridDim.x * tid;
+        const bool tie = i < p.B && p.status[i] == DSP_CLIP_UNCERTIFIED;
+        if (tid == 0) sh->next = 0;
         __syncthreads();
+        if (tie) list[atomicAdd(&sh->next, 1)] = (int)i;
+        __syncthreads();
+        const int nt = sh->next;
+        for (int t = 0; t < nt; t++) {
+            const int ci = list[t];
+            if (!built) {
+                build_window(p, c, tid, lane, wid);
+                built = true;
+            }
+            c.stamp_clip = ci;
+            const ClipRef cr = clip_ref(p, ci);
+            short8 regs[NRV];
+            issue_clip(regs, p, cr);
+            clip_body<true, FAST>(p, c, ci, cr, regs);
+            __syncthreads();
+        }
     }
 }
 
@@ -1676,7 +1693,8 @@ extern "C" size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int f
     if (max_len < 1 || frame_length < 1 || frame_shift < 1) return 0;
     if (max_len > (1 << 24) || frame_length > (1 << 20)) return 0;
     const ExtractCarve c = extract_carve((int)max_len, frame_length, frame_shift);
-    return c.total <= EXTRACT_LDS_LIMIT ? (size_t)c.total : 0;
+    // + the exact kernel's list of near ties (4 bytes per thread past the layout)
+    return c.total + 4 * EXTRACT_THREADS <= EXTRACT_LDS_LIMIT ? (size_t)c.total : 0;
 }
 
 // CU count per device (the persistent grid), cached on first use of each device
@@ -1756,10 +1774,10 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
 #else
         hipLaunchKernelGGL(dsp::extract_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
 #endif
-        hipLaunchKernelGGL(dsp::extract_exact_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
+        hipLaunchKernelGGL(dsp::extract_exact_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch + 4 * dsp::NT, s, p);
     } else {
         hipLaunchKernelGGL(dsp::extract_kernel<false>, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
-        hipLaunchKernelGGL(dsp::extract_exact_kernel<false>, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
+        hipLaunchKernelGGL(dsp::extract_exact_kernel<false>, dim3(grid), dim3(dsp::NT), lds_launch + 4 * dsp::NT, s, p);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? DSP_OK : DSP_ERR_HIP + (int)e;
