@@ -132,7 +132,9 @@ struct Shared {
     double noise_e, noise_z;  // VAD noise estimates (:189-195, :239-245)
     double oslo[3], oshi[3];  // order statistics (F-1)/2 and F/2 of E, M, ZCR (medians)
     int n3, n1, n6, exact, j0, j1, next;
-    int qnext, qend, qcursor;  // clip queue (thread 0): the current chunk's next clip and end; static split
+    int qnext, qend, qcursor, qrange;  // clip queue (thread 0): the current chunk's next clip and end;
+                                       // static split cursor; ranges used up
+    int cdir, cy;                      // the pending claim (queue_begin / queue_end)
 };
 static_assert(sizeof(Shared) <= EXTRACT_SHARED_BYTES, "grow EXTRACT_SHARED_BYTES");
 
@@ -918,15 +920,114 @@ __device__ __forceinline__ void r5_fast(const Ctx &c, int F, float *featb, int w
     }
 }
 
+// Clip queue (ABI 3).  p.queue: the caller's zeroed 64-byte scratch, words 0-7 the claim counters
+// of eight ranges of clip chunks (EXTRACT_CHUNK consecutive clips each; range x = the chunks
+// [x nch / 8, (x + 1) nch / 8)), word 8 the count of workgroups done.  A workgroup claims chunks
+// from the range of the XCD it runs on (HW_REG_XCC_ID: placement is a performance matter only,
+// any id is correct), then from the others in turn once its own is exhausted: one atomic per chunk
+// instead of per clip, consecutive clips on one XCD -- their 76-B output rows share cache lines in
+// that XCD's L2 instead of leaving it as partial-line writes -- and fast workgroups take more
+// chunks (a static i, i + G, ... split ends on the slowest workgroup: 3.19-3.98 ms spread at
+// 100 000 clips).  p.queue == NULL: the static split.  Thread 0 only.
+#ifndef EXTRACT_CHUNK
+#define EXTRACT_CHUNK 4
+#endif
+#ifndef EXTRACT_XCD_RANGES
+#define EXTRACT_XCD_RANGES 8  // 1: one range for every workgroup (A/B)
+#endif
+static_assert(EXTRACT_XCD_RANGES >= 1 && EXTRACT_XCD_RANGES <= 8, "queue_ws holds 8 range counters");
+struct ClipQueue {  // wave-uniform; the mutable state lives in Shared (thread 0 only)
+    unsigned *q;
+    int B, nch, xcd;
+};
+__device__ __forceinline__ ClipQueue queue_open(const ExtractParams &p, Shared *sh)
+{
+    ClipQueue Q;
+    Q.q = p.queue;
+    Q.B = p.B;
+    Q.nch = (p.B + EXTRACT_CHUNK - 1) / EXTRACT_CHUNK;
+    Q.xcd = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;  // HW_REG_XCC_ID[3:0]
+    if (threadIdx.x == 0) {
+        sh->qnext = sh->qend = sh->qrange = 0;
+        sh->qcursor = (int)blockIdx.x - (int)gridDim.x;
+    }
+    return Q;
+}
+// Claiming is split so that the counter's atomic never stalls the clip: queue_begin (at the clip's
+// start, right after its loads) issues the atomic when the current chunk is used up, and
+// queue_end (before R5) consumes its result.  The vmcnt counter is in order, so a wait for an
+// atomic issued after the clip's loads would also wait for those loads.  Thread 0 only.
+// The pending claim's state sits in LDS (sh->cdir: the next clip, -1, or -2 = pending on the
+// atomic; sh->cy: its range); only the atomic's return value stays in a register.
+__device__ __forceinline__ unsigned queue_begin(const ClipQueue &Q, Shared *sh)
+{
+    if (!Q.q) {
+        const int t = sh->qcursor + (int)gridDim.x;
+        sh->qcursor = t;
+        sh->cdir = t < Q.B ? t : -1;
+        return 0;
+    }
+    const int nx = sh->qnext;
+    if (nx < sh->qend) {
+        sh->qnext = nx + 1;
+        sh->cdir = nx;
+        return 0;
+    }
+    if (sh->qrange >= EXTRACT_XCD_RANGES) {  // every range exhausted
+        sh->cdir = -1;
+        return 0;
+    }
+    const int y = (Q.xcd + sh->qrange) % EXTRACT_XCD_RANGES;
+    sh->cy = y;
+    sh->cdir = -2;
+    return __hip_atomic_fetch_add(Q.q + y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int queue_end(const ClipQueue &Q, Shared *sh, unsigned ret)
+{
+    constexpr int NR = EXTRACT_XCD_RANGES;
+    if (sh->cdir != -2) return sh->cdir;
+    int y = sh->cy;
+    for (;;) {
+        const unsigned c0 = (unsigned)(y * Q.nch / NR), c1 = (unsigned)((y + 1) * Q.nch / NR);
+        if (c0 + ret < c1) {
+            const int first = (int)(c0 + ret) * EXTRACT_CHUNK;
+            sh->qnext = first + 1;
+            sh->qend = min(Q.B, first + EXTRACT_CHUNK);
+            return first;
+        }
+        // this range is used up: the next one (a blocking claim, rare: the end of the launch)
+        const int r = ++sh->qrange;
+        if (r >= NR) return -1;
+        y = (Q.xcd + r) % NR;
+        ret = __hip_atomic_fetch_add(Q.q + y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+__device__ __forceinline__ int queue_next(const ClipQueue &Q, Shared *sh) { return queue_end(Q, sh, queue_begin(Q, sh)); }
+// the last workgroup out resets the queue for the next launch on the stream: every claim of every
+// workgroup precedes its increment of the done count.  Thread 0 only.
+__device__ __forceinline__ void queue_done(const ExtractParams &p)
+{
+    if (!p.queue) return;
+    const unsigned d = __hip_atomic_fetch_add(p.queue + 8, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == gridDim.x - 1) {
+#pragma unroll
+        for (int y = 0; y < 8; y++) __hip_atomic_store(p.queue + y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p.queue + 8, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // One clip, start to finish; its first RREG words are already in flight into regs (word
 // r * NT + tid in regs[4r .. 4r+3]).  EXACT = false: endpoint energies from exact moments,
 // decisions certified; returns false on a near tie (the clip is then redone with EXACT = true
 // after the persistent loop).
 // FAST: the compile-time LDS layout (extract_carve_fast); the clip is in registers and there are
 // at most 128 VAD and feature frames, so the long-clip paths drop out
-template <bool EXACT, bool FAST>
+struct NoClaim {
+    __device__ int operator()() const { return -1; }
+};
+template <bool EXACT, bool FAST, typename Resolve = NoClaim>
 __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, int i, const ClipRef &cur,
-                                          short8 (&regs)[NRV], int claim = -1)
+                                          short8 (&regs)[NRV], Resolve resolve = NoClaim())
 {
     Shared *sh = c.sh;
     const int tid = opaque_tid(), lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
@@ -1140,7 +1241,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     if (!FAST && F > 128)
         for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
     if constexpr (!EXACT)
-        if (tid == 0) sh->next = claim;  // claimed at the clip's start (-1: none)
+        if (tid == 0) sh->next = resolve();  // claimed at the clip's start (-1: none)
     __syncthreads();
     if constexpr (!EXACT) {
         // regs are dead since R2: the next clip's words load while R5 runs (unconditional, a
@@ -1313,79 +1414,6 @@ __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &
     __syncthreads();
 }
 
-// Clip queue (ABI 3).  p.queue: the caller's zeroed 64-byte scratch, words 0-7 the claim counters
-// of eight ranges of clip chunks (EXTRACT_CHUNK consecutive clips each; range x = the chunks
-// [x nch / 8, (x + 1) nch / 8)), word 8 the count of workgroups done.  A workgroup claims chunks
-// from the range of the XCD it runs on (HW_REG_XCC_ID: placement is a performance matter only,
-// any id is correct), then from the others in turn once its own is exhausted: one atomic per chunk
-// instead of per clip, consecutive clips on one XCD -- their 76-B output rows share cache lines in
-// that XCD's L2 instead of leaving it as partial-line writes -- and fast workgroups take more
-// chunks (a static i, i + G, ... split ends on the slowest workgroup: 3.19-3.98 ms spread at
-// 100 000 clips).  p.queue == NULL: the static split.  Thread 0 only.
-#ifndef EXTRACT_CHUNK
-#define EXTRACT_CHUNK 4
-#endif
-#ifndef EXTRACT_XCD_RANGES
-#define EXTRACT_XCD_RANGES 8  // 1: one range for every workgroup (A/B)
-#endif
-struct ClipQueue {  // wave-uniform; the mutable state lives in Shared (thread 0 only)
-    unsigned *q;
-    int B, nch, xcd;
-};
-__device__ __forceinline__ ClipQueue queue_open(const ExtractParams &p, Shared *sh)
-{
-    ClipQueue Q;
-    Q.q = p.queue;
-    Q.B = p.B;
-    Q.nch = (p.B + EXTRACT_CHUNK - 1) / EXTRACT_CHUNK;
-    Q.xcd = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;  // HW_REG_XCC_ID[3:0]
-    if (threadIdx.x == 0) {
-        sh->qnext = sh->qend = 0;
-        sh->qcursor = (int)blockIdx.x - (int)gridDim.x;
-    }
-    return Q;
-}
-// the next clip of this workgroup, -1 when none is left.  Thread 0 only.
-__device__ __forceinline__ int queue_next(const ClipQueue &Q, Shared *sh)
-{
-    if (!Q.q) {
-        const int c = sh->qcursor + (int)gridDim.x;
-        sh->qcursor = c;
-        return c < Q.B ? c : -1;
-    }
-    const int nx = sh->qnext;
-    if (nx < sh->qend) {
-        sh->qnext = nx + 1;
-        return nx;
-    }
-    constexpr int NR = EXTRACT_XCD_RANGES;
-    for (int t = 0; t < NR; t++) {
-        const int y = (Q.xcd + t) % NR;
-        const unsigned c0 = (unsigned)(y * Q.nch / NR), c1 = (unsigned)((y + 1) * Q.nch / NR);
-        // a relaxed look first: exhausted ranges cost no atomic
-        if (c0 + __hip_atomic_load(Q.q + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= c1) continue;
-        const unsigned c = c0 + __hip_atomic_fetch_add(Q.q + y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (c < c1) {
-            const int first = (int)c * EXTRACT_CHUNK;
-            sh->qnext = first + 1;
-            sh->qend = min(Q.B, first + EXTRACT_CHUNK);
-            return first;
-        }
-    }
-    return -1;
-}
-// the last workgroup out resets the queue for the next launch on the stream: every claim of every
-// workgroup precedes its increment of the done count.  Thread 0 only.
-__device__ __forceinline__ void queue_done(const ExtractParams &p)
-{
-    if (!p.queue) return;
-    const unsigned d = __hip_atomic_fetch_add(p.queue + 8, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (d == gridDim.x - 1) {
-#pragma unroll
-        for (int y = 0; y < 8; y++) __hip_atomic_store(p.queue + y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(p.queue + 8, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
 
 // FAST launches: 0 = extract_kernel<true> (one clip at a time per workgroup), 1 = the two-clip
 // pipeline extract_pipe_kernel.  The pipeline overlaps the single-wave phases of one clip with the
@@ -1423,21 +1451,25 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     bool inflight = false;  // regs already hold clip i's loads (issued by the previous clip's R4)
     for (int i = sh->next; i >= 0;) {
         const ClipRef cur = clip_ref(p, i);
-        int claim = -1;
         if (!cur.ok) {
             __syncthreads();  // everyone has read sh->next (the ok path has barriers in clip_body)
-            if (tid == 0) claim = queue_next(Q, sh);
+            if (tid == 0) sh->next = queue_next(Q, sh);
             write_bad_clip(p, i, tid);
             inflight = false;
         } else {
             if (!inflight) issue_clip(regs, p, cur);
-            if (tid == 0) claim = queue_next(Q, sh);
+            unsigned cl = 0;
+            if (tid == 0) cl = queue_begin(Q, sh);
             c.stamp_clip = i;
-            const bool done = clip_body<false, FAST>(p, c, i, cur, regs, claim);
-            if (!done && tid == 0) p.status[i] = DSP_CLIP_UNCERTIFIED;
-            inflight = done;  // a deferred clip returns before R4
+            const bool done = clip_body<false, FAST>(p, c, i, cur, regs, [&]() { return queue_end(Q, sh, cl); });
+            if (!done) {  // a deferred clip returns before R4
+                if (tid == 0) {
+                    p.status[i] = DSP_CLIP_UNCERTIFIED;
+                    sh->next = queue_end(Q, sh, cl);
+                }
+            }
+            inflight = done;
         }
-        if (tid == 0) sh->next = claim;
         __syncthreads();  // LDS summaries are rewritten by the next clip; sh->next published
         i = sh->next;
     }
