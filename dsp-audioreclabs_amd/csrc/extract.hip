@@ -42,12 +42,6 @@
 #ifndef DSP_ABL  // diagnostic ablation builds only (tools/ablate_build.sh; outputs are wrong): skip
 #define DSP_ABL 0 // 1 = R4 frames, 2 = R5 jobs, 4 = R2 sign bits, 8 = VAD pass-A partial moments
 #endif
-#ifndef EXTRACT_R4_KV
-#define EXTRACT_R4_KV 9   // vectors per lane per unrolled R4 step (a multiple of EXTRACT_R4_PF)
-#endif
-#ifndef EXTRACT_R4_PF
-#define EXTRACT_R4_PF 9   // R4 crop loads in flight per lane: a whole 1102-sample frame (RUN 1)
-#endif
 
 namespace dsp {
 
@@ -65,12 +59,6 @@ static constexpr int NRV = 4 * RREG;       // 16-B vectors per thread in registe
     } while (0)
 // per workgroup (row blockIdx.x, slots 16..): real-time and shader-clock stamps (WG_STAMP, at
 // entry and exit) and shader-clock stamps inside the prologue (WG_CK)
-// the pipelined kernel: lane 0 of wave w stamps slot k of clip row `clip`
-#define STAMPW(clip, k, w)                                                                       \
-    do {                                                                                         \
-        if (threadIdx.x == 64 * (w) && p.stamps && (clip) >= 0)                                  \
-            p.stamps[(size_t)(clip) * 32 + (k)] = __builtin_amdgcn_s_memtime();                  \
-    } while (0)
 #define WG_STAMP(k)                                                                          \
     do {                                                                                     \
         if (threadIdx.x == 0 && p.stamps) {                                                  \
@@ -91,9 +79,6 @@ static constexpr int NRV = 4 * RREG;       // 16-B vectors per thread in registe
     } while (0)
 #define STAMP(clip, k) \
     do {               \
-    } while (0)
-#define STAMPW(clip, k, w) \
-    do {                   \
     } while (0)
 #endif
 
@@ -167,7 +152,7 @@ __device__ __forceinline__ ClipRef clip_none()
 
 struct Ctx {
     Shared *sh;
-    const float *wtab;  // EXTRACT_WROW(L) floats per shifted copy r = 0..3 (extract_layout.h)
+    const float *wtab;  // window table: 2 copies of EXTRACT_WCOPY(L) bytes (extract_layout.h)
     uint32_t *posw;      // bit u of the buffer: sample u is real and positive after preprocess
     unsigned long long *wS2;
     int *wS1;
@@ -178,6 +163,7 @@ struct Ctx {
     int *rank;  // rank scratch: nvcap or 3 * fcap ints
     int *pS1;   // partial-word moments at the two ends of each VAD frame (2 * nvcap)
     unsigned long long *pS2;
+    float2v *part;  // R4: the 8 octet sums {E, M} of each feature frame
     int64_t total;
     int stamp_clip;  // clip index for the diagnostic stamps
 };
@@ -742,133 +728,198 @@ __device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur
     }
 }
 
-// R4: windowed frames over the crop [st, en) (:378, :299-333; fe.py:12-43) -> c.fE / fM / fZ.
-// A 16-lane row takes a RUN of EXTRACT_R4_RUN consecutive frames; its lanes walk the run's
-// clip-relative 8-sample vectors in the canonical clip-absolute order of dsp_device.h (lane rl:
-// the vectors v = rl mod 16, re-read from L2 by 16-B loads at the clip's own 2-byte alignment),
-// so each vector is loaded and turned into (x^2, |x|) once for every frame of the run that holds
-// it, and the sums equal dsp_extract_general's (position independent).  Per frame and sample pair
+// R4: windowed frames over the crop [st, en) (:378, :299-333; fe.py:12-43) -> c.fE / fM / fZ, in
+// the canonical order of dsp_device.h (lane l = class l).  The waves split the F frames into
+// contiguous ranges; a wave walks the 64-vector steps its frames cover (lane l: clip vector
+// 64 t + l, re-read from L2 by a 16-B load at the clip's own 2-byte alignment), turns each vector
+// into (x^2, |x|) once and adds it into every frame open in the step, up to R4_NSLOT at a time:
+// frame f0 + (s + R4_NSLOT j) G sits in slot s, G = r4_sweeps(L, S) sweeps (g: frames f0 + g + jG)
+// so that a slot's next frame never opens before its frame closes.  Per frame and sample pair
 // e = fma(w^2, x^2, e), m = fma(w, |x|, m); the 8 (w, w^2) pairs of a vector are four aligned 16-B
-// reads from the window table copy of the right parity.  Runs go four to a wave (one per row),
-// run group g to the wave of rank (wrank) g mod NWAVE.  Returns F.
-#ifndef EXTRACT_R4_RUN
-#define EXTRACT_R4_RUN 1
+// reads from the window table copy of the frame's parity (a vector wholly outside the window
+// reads a zero run: clamped element index).  A frame that closes is folded into its 8 octet sums
+// (c.part); after a barrier, four lanes per frame add them in order and count its sign changes.
+#define R4_NSLOT 4
+#ifndef R4_PF
+#define R4_PF 2  // 64-vector steps loaded ahead
 #endif
-__device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int st, int en,
-                                         const ClipStats &cs, int j0, int j1, int wrank, int lane)
+__host__ __device__ constexpr int r4_sweeps(int L, int S)
 {
-    constexpr int RUN = EXTRACT_R4_RUN;
-    constexpr int KV = EXTRACT_R4_KV;  // vectors per lane in one batch
+    // slot reuse: frame f + NSLOT G opens at least one step after frame f's last sample
+    return (L + 511 + R4_NSLOT * S - 1) / (R4_NSLOT * S);
+}
+__device__ __forceinline__ int med3_i(int x, int lo, int hi)
+{
+    int r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "s"(hi));
+    return r;
+}
+template <bool NEAR0>
+__device__ __forceinline__ void r4_sweep(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int st, int en,
+                                         int L, int S, int G, int f0, int fb, const CanonX &cx, int vfix,
+                                         short klast, int lane)
+{
+    const int flast = f0 + ((fb - 1 - f0) / G) * G;  // the sweep's frames f0, f0 + G, .. flast
+    const int ta = (st + f0 * S) >> 9, tb = (min(st + flast * S + L, en) - 1) >> 9;
+    const int wcopy = EXTRACT_WCOPY(L), rmax = EXTRACT_WRMAX(L);
+    const int n = cur.n;
+    // slot s: its frame fi (first sample fsm), the steps it opens and closes in, and where lane l's
+    // vector at step t starts in the window table: pair slot 4 (l + 64 t + U) + s0 of the copy at
+    // byte offset wb (rows 80 B apart, extract_layout.h)
+    int fi[R4_NSLOT], fsm[R4_NSLOT], topen[R4_NSLOT], tclose[R4_NSLOT], U[R4_NSLOT], s0[R4_NSLOT], wb[R4_NSLOT];
+    float2v e[R4_NSLOT], mm[R4_NSLOT];
+    auto derive = [&](int s) {  // from fi[s] and fsm[s]
+        const int r = fsm[s] & 1;
+        const bool in = fi[s] <= flast;
+        topen[s] = in ? fsm[s] >> 9 : 0x7fffffff;
+        tclose[s] = in ? (min(fsm[s] + L, en) - 1) >> 9 : -1;
+        const int c2 = (EXTRACT_WPAD + r - fsm[s]) >> 1;  // exact: WPAD + r - fsm is even
+        U[s] = c2 >> 2;
+        s0[s] = c2 & 3;
+        wb[s] = r ? wcopy : 0;
+    };
+    const int fstep = R4_NSLOT * G, sstep = R4_NSLOT * G * S;
+#pragma unroll
+    for (int s = 0; s < R4_NSLOT; s++) {
+        fi[s] = f0 + s * G;
+        fsm[s] = st + fi[s] * S;
+        derive(s);
+        e[s] = mm[s] = (float2v){0.f, 0.f};
+    }
+    const unsigned char *wt = reinterpret_cast<const unsigned char *>(c.wtab);
+    const int zero = 0;
+    auto step = [&](int t, const short8 &xv) {
+        const int v = 64 * t + lane;
+        float2v q[4], a[4];
+        if (512 * t + 512 >= en) {  // the crop's last step: samples from en on are frame_signal's zero padding
+            short8 k = xv;
+            if (vfix >= 0 && v == vfix) k[(n - 1) & 7] = klast;
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+                float2v x = canon_x2<NEAR0>(k[2 * h], k[2 * h + 1], cx);
+                const int u = 8 * v + 2 * h;
+                x.x = u < en ? x.x : 0.f;
+                x.y = u + 1 < en ? x.y : 0.f;
+                canon_qa(x, q[h], a[h]);
+            }
+        } else {
+#pragma unroll
+            for (int h = 0; h < 4; h++) canon_qa(canon_x2<NEAR0>(xv[2 * h], xv[2 * h + 1], cx), q[h], a[h]);
+        }
+#pragma unroll
+        for (int s = 0; s < R4_NSLOT; s++) {
+            if (t >= topen[s]) {  // open (a slot is reassigned when its frame closes)
+                // row clamped to the zero rows: a vector wholly outside the window reads zeros
+                const int R = med3_i(lane + (U[s] + 64 * t), zero, rmax);
+                const float4 *rp = reinterpret_cast<const float4 *>(wt + wb[s]) + 5 * R;  // 80-B rows
+                // pair h at slot s0 + h of the row (next row from slot 4 on: +16 B of row padding)
+                auto acc = [&](auto s0t) {
+                    constexpr int S0 = decltype(s0t)::value;
+#pragma unroll
+                    for (int h = 0; h < 4; h++) {
+                        const float4 ww = rp[S0 + h + (S0 + h >= 4 ? 1 : 0)];
+                        canon_acc((float2v){ww.x, ww.y}, (float2v){ww.z, ww.w}, q[h], a[h], e[s], mm[s]);
+                    }
+                    // a distinct marker per phase keeps the four variants apart (merged, their
+                    // immediate offsets would become per-dword address arithmetic)
+                    asm volatile("; r4 phase %0" ::"n"(S0));
+                };
+                switch (s0[s]) {
+                case 0: acc(IntT<0>()); break;
+                case 1: acc(IntT<1>()); break;
+                case 2: acc(IntT<2>()); break;
+                default: acc(IntT<3>()); break;
+                }
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < R4_NSLOT; s++) {
+            if (t == tclose[s]) {
+                float eo = e[s].x + e[s].y, mo = mm[s].x + mm[s].y;
+                r4_octet2(eo, mo);
+                c.part[8 * fi[s] + (lane >> 3)] = (float2v){eo, mo};
+                e[s] = mm[s] = (float2v){0.f, 0.f};
+                fi[s] += fstep;
+                fsm[s] += sstep;
+                derive(s);
+            }
+        }
+    };
+    // R4_PF steps' vectors in flight
+    short8 xr[R4_PF];
+#pragma unroll
+    for (int k = 0; k < R4_PF; k++) xr[k] = load_cvec(p, cur, 64 * (ta + k) + lane);
+    for (int t = ta; t <= tb; t += R4_PF) {
+#pragma unroll
+        for (int k = 0; k < R4_PF; k++) {
+            if (k == 0 || t + k <= tb) {
+                step(t + k, xr[k]);
+                xr[k] = load_cvec(p, cur, 64 * (t + k + R4_PF) + lane);
+            }
+        }
+    }
+}
+
+// the frame sums in canonical order (octets 0..7 from the left) and the ZCR: four lanes per frame
+__device__ __forceinline__ void r4_finish(const Ctx &c, int st, int en, int L, int S, int F, int j0, int j1, int lead,
+                                          float sE, float sM, int tid)
+{
+    for (int b = 0; b < F; b += NT / 4) {
+        const int f = b + (tid >> 2), lq = tid & 3;
+        const bool act = f < F;
+        const int fs = st + (act ? f : 0) * S;
+        // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in [j0, j1])
+        // and before the crop end; transitions into the window's zero ends / padding count too
+        const int ia = fs + j0, ib = min(fs + j1, en - 1);  // sample coords
+        int z = dpp_quad_reduce((act && ia < ib) ? chg_count(c.posw, ia + lead, ib + lead, lq, 4) : 0, OpAdd());
+        if (act && lq == 0) {
+            if (ia <= ib) {
+                if (j0 > 0) z += pos_bit(c.posw, ia + lead);
+                if (ib < fs + L - 1) z += pos_bit(c.posw, ib + lead);
+            }
+            float oe[8], om[8];
+            const float4 *pp = reinterpret_cast<const float4 *>(c.part + 8 * f);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const float4 u = pp[k];
+                oe[2 * k] = u.x;
+                om[2 * k] = u.y;
+                oe[2 * k + 1] = u.z;
+                om[2 * k + 1] = u.w;
+            }
+            c.fE[f] = r4_sum8(oe) * sE;
+            c.fM[f] = r4_sum8(om) * sM;
+            c.fZ[f] = z;
+        }
+    }
+}
+
+// Returns F.  Ends with a barrier.
+__device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int st, int en,
+                                         const ClipStats &cs, int j0, int j1, int wrank, int tid)
+{
     const int L = p.L, S = p.S, n = cur.n, lead = cur.lead;
     const int m = en - st;  // > 0 always (start < end)
     const int F = (m <= L) ? 1 : (m - L + S - 1) / S + 1;
-    const int nrun = (F + RUN - 1) / RUN;
-    const float sE = cs.invMf * cs.invMf, sM = cs.invMf;
-    const int wrow = EXTRACT_WROW(L);
+    const int G = r4_sweeps(L, S);
     const CanonX cx = canon_x(cs.mq, cs.t0);
     // a 16-B load ending past the clip's last buffer vector drops a dword that straddles the
     // descriptor's end (range checks are per dword): with an odd lead and a clip ending on a
     // vector boundary that dword holds the last sample, patched in from the aligned vector
     const int vfix = ((lead & 1) && ((lead + n) & 7) == 0) ? (n - 1) >> 3 : -1;
     const short klast = vfix >= 0 ? load_vec(p, cur, cur.nvec - 1)[7] : (short)0;
-    const int rl = lane & 15, row = lane >> 4;
-    // the run of this lane's row in run group gi: frames g0 .. g0 + RUN - 1 (those < F), vectors
-    // [va, vb]; the lane's first vector v0 (= rl mod 16)
-    auto run_geom = [&](int gi, int &g0, int &va, int &vb, int &v0) {
-        const int run = 4 * gi + row;
-        g0 = RUN * (run < nrun ? run : nrun - 1);
-        const int gl = min(g0 + RUN, F) - 1;
-        const int fs0 = st + g0 * S, fsl = st + gl * S;
-        va = fs0 >> 3;
-        vb = (fsl + min(L, en - fsl) - 1) >> 3;
-        v0 = canon_first(va, rl);
-    };
-    for (int gi = wrank; !(DSP_ABL & 1) && 4 * gi < nrun; gi += NWAVE) {
-        const bool act = 4 * gi + row < nrun;
-        int g0, va, vb, v0;
-        run_geom(gi, g0, va, vb, v0);
-        int fs[RUN];
-        bool in[RUN];
-#pragma unroll
-        for (int j = 0; j < RUN; j++) {
-            in[j] = g0 + j < F;
-            fs[j] = st + (g0 + j) * S;
-        }
-        float2v e[RUN], mm[RUN];
-#pragma unroll
-        for (int j = 0; j < RUN; j++) e[j] = mm[j] = (float2v){0.f, 0.f};
-        // samples at or past the crop end en are the zero padding of frame_signal: their x is set
-        // to 0 (fma(w^2, 0, e) = e, the bits of a zero weight) -- only rows whose run reaches en
-        const bool padded = 8 * vb + 8 > en;
-        for (int vb0 = v0; vb0 <= vb; vb0 += 16 * KV) {
-            short8 xv[KV];
-#pragma unroll
-            for (int k = 0; k < KV; k++) xv[k] = load_cvec(p, cur, vb0 + 16 * k);
-            if (vfix >= 0)  // clip-uniform, rare
-#pragma unroll
-                for (int k = 0; k < KV; k++)
-                    if (vb0 + 16 * k == vfix) xv[k][(n - 1) & 7] = klast;
-            auto run = [&](auto pad_t, auto near_t) {
-                constexpr bool PADDED = decltype(pad_t)::value, NEAR0 = decltype(near_t)::value;
-#pragma unroll
-                for (int k = 0; k < KV; k++) {
-                    const int v = vb0 + 16 * k;
-                    if (v > vb) continue;
-                    float2v q[4], a[4];
-#pragma unroll
-                    for (int h = 0; h < 4; h++) {
-                        float2v x = canon_x2<NEAR0>(xv[k][2 * h], xv[k][2 * h + 1], cx);
-                        if (PADDED) {
-                            const int u = 8 * v + 2 * h;  // clip sample of the pair's first element
-                            x.x = u < en ? x.x : 0.f;
-                            x.y = u + 1 < en ? x.y : 0.f;
-                        }
-                        canon_qa(x, q[h], a[h]);
-                    }
-#pragma unroll
-                    for (int j = 0; j < RUN; j++) {
-                        const int jb = 8 * v - fs[j];  // window index of the vector's first sample
-                        if (RUN > 1 && (!in[j] || jb <= -8 || jb >= L)) continue;
-                        // copy r = jb & 1, pair slot (jb + WPAD + r) / 2: {w, w, w^2, w^2} of the
-                        // samples jb + 2h, jb + 2h + 1 at slot + h
-                        const int r = jb & 1;
-                        const float4 *wp = reinterpret_cast<const float4 *>(c.wtab) + r * (wrow / 2) +
-                                           ((jb + EXTRACT_WPAD + r) >> 1);
-#pragma unroll
-                        for (int h = 0; h < 4; h++) {
-                            const float4 ww = wp[h];
-                            canon_acc((float2v){ww.x, ww.y}, (float2v){ww.z, ww.w}, q[h], a[h], e[j], mm[j]);
-                        }
-                    }
-                }
-            };
-            if (padded)
-                cx.near0 ? run(BoolT<true>(), BoolT<true>()) : run(BoolT<true>(), BoolT<false>());
-            else if (cx.near0)
-                run(BoolT<false>(), BoolT<true>());
+    const int lane = tid & 63;
+    const int fa = (F * wrank) / NWAVE, fb = (F * (wrank + 1)) / NWAVE;  // this wave's frames
+    if (!(DSP_ABL & 1))
+        for (int g = 0; g < G && fa + g < fb; g++) {
+            if (cx.near0)
+                r4_sweep<true>(p, c, cur, st, en, L, S, G, fa + g, fb, cx, vfix, klast, lane);
             else
-                run(BoolT<false>(), BoolT<false>());
+                r4_sweep<false>(p, c, cur, st, en, L, S, G, fa + g, fb, cx, vfix, klast, lane);
         }
-#pragma unroll
-        for (int j = 0; j < RUN; j++) {
-            const float E1 = dpp_row_reduce(e[j].x + e[j].y, OpAdd()) * sE;
-            const float M1 = dpp_row_reduce(mm[j].x + mm[j].y, OpAdd()) * sM;
-            // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in
-            // [j0, j1]) and before the crop end; transitions into the window's zero ends /
-            // padding count too
-            const int ia = fs[j] + j0, ib = min(fs[j] + j1, en - 1);  // sample coords
-            int z = dpp_row_reduce((in[j] && ia < ib) ? chg_count(c.posw, ia + lead, ib + lead, rl, 16) : 0, OpAdd());
-            if (ia <= ib) {
-                if (j0 > 0) z += pos_bit(c.posw, ia + lead);
-                if (ib < fs[j] + L - 1) z += pos_bit(c.posw, ib + lead);
-            }
-            if (act && in[j] && rl == 0) {
-                c.fE[g0 + j] = E1;
-                c.fM[g0 + j] = M1;
-                c.fZ[g0 + j] = z;
-            }
-        }
-    }
+    __syncthreads();
+    const float sE = cs.invMf * cs.invMf, sM = cs.invMf;
+    r4_finish(c, st, en, L, S, F, j0, j1, lead, sE, sM, tid);
     return F;
 }
 
@@ -1236,7 +1287,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     STAMP(i, 4);
 
     // ---- R4: windowed frames over the crop [st, en) (r4_frames) --------------------------------
-    const int F = r4_frames(p, c, cur, st, en, cs, sh->j0, sh->j1, wid, lane);
+    const int F = r4_frames(p, c, cur, st, en, cs, sh->j0, sh->j1, wid, tid);
     STAMP(i, 12);
     if (!FAST && F > 128)
         for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
@@ -1348,6 +1399,7 @@ __device__ __forceinline__ Ctx ctx_from(const ExtractCarve &cv, unsigned char *l
     c.rank = reinterpret_cast<int *>(lds + cv.rank);
     c.pS1 = reinterpret_cast<int *>(lds + cv.pS1);
     c.pS2 = reinterpret_cast<unsigned long long *>(lds + cv.pS2);
+    c.part = reinterpret_cast<float2v *>(lds + cv.part);
     c.total = 0;
     c.stamp_clip = 0;
     return c;
@@ -1369,7 +1421,7 @@ __device__ __forceinline__ Ctx make_ctx(const ExtractParams &p, unsigned char *l
 // with a barrier.
 __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &c, int tid, int lane, int wid)
 {
-    float *wt = const_cast<float *>(c.wtab);  // 2 copies of wrow (w, w^2) pairs
+    unsigned char *wt = reinterpret_cast<unsigned char *>(const_cast<float *>(c.wtab));  // 2 copies
     Shared *sh = c.sh;
     const int L = p.L;
     constexpr int WPRE = 3;
@@ -1383,12 +1435,8 @@ __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &
         sh->j0 = L;
         sh->j1 = -1;
     }
-    const int wrow = EXTRACT_WROW(L);
-    // copy r (0, 1), pair slot i = {w_a, w_a+1, w2_a, w2_a+1} of window indices a = 2i - WPAD - r
-    // (zero outside [0, L)): the 8 (w, w^2) of a vector starting at any window index are four
-    // aligned 16-B reads from the copy of that index's parity, already in register-pair order
-    for (int t = tid; t < 2 * wrow; t += NT) wt[(t / wrow) * 2 * wrow + 2 * (t % wrow) + 0] = 0.f;
-    for (int t = tid; t < 2 * wrow; t += NT) wt[(t / wrow) * 2 * wrow + 2 * (t % wrow) + 1] = 0.f;
+    const int wcopy = EXTRACT_WCOPY(L);
+    for (int t = tid; t < wcopy / 2; t += NT) reinterpret_cast<float *>(wt)[t] = 0.f;  // both copies
     __syncthreads();
     auto put_weight = [&](int q0, double w) {  // weight j = q0 + lane (q0 wave-uniform)
         const int j = q0 + lane;
@@ -1397,9 +1445,11 @@ __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &
             const float wf = (float)w;
 #pragma unroll
             for (int r = 0; r < 2; r++) {
-                const int m = j + EXTRACT_WPAD + r;  // slot m >> 1, position m & 1
-                wt[r * 2 * wrow + 4 * (m >> 1) + (m & 1)] = wf;
-                wt[r * 2 * wrow + 4 * (m >> 1) + 2 + (m & 1)] = canon_w2(wf);
+                const int m = j + EXTRACT_WPAD + r;  // slot P = m >> 1, position m & 1
+                const int P = m >> 1;
+                float *slot = reinterpret_cast<float *>(wt + r * wcopy + 80 * (P >> 2) + 16 * (P & 3));
+                slot[m & 1] = wf;
+                slot[2 + (m & 1)] = canon_w2(wf);
             }
         }
         const unsigned long long m = __ballot(in && w > 0.0);
@@ -1415,17 +1465,10 @@ __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &
 }
 
 
-// FAST launches: 0 = extract_kernel<true> (one clip at a time per workgroup), 1 = the two-clip
-// pipeline extract_pipe_kernel.  The pipeline overlaps the single-wave phases of one clip with the
-// multi-wave phases of the other, but the CU is bound by instruction issue (about one issuing wave
-// per SIMD per 4-cycle slot at 100 000 clips), and the pipeline adds 10% VALU and 49% SALU
-// instructions: 3.41 against 3.35 ms (profiles/r04d_*), so the one-clip loop ships.
-#ifndef EXTRACT_PIPE
-#define EXTRACT_PIPE 0
-#endif
-#if !EXTRACT_PIPE
-#define EXTRACT_PIPE_UNUSED __attribute__((unused))
-#endif
+// FAST launches run extract_kernel<true>, one clip at a time per workgroup.  A two-clip pipeline
+// (the single-wave phases of one clip beside the multi-wave phases of the other, round 4) measured
+// 3.41 against 3.35 ms: the CU is bound by instruction issue and the pipeline added 10% VALU and
+// 49% SALU instructions (profiles/r04d_*), so it was removed.
 
 // 128 VGPRs: two 512-thread workgroups per CU
 #ifndef EXTRACT_WAVES_PER_EU
@@ -1477,201 +1520,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     WG_STAMP(22);
 }
 
-// ---- FAST layout: two clips in flight per workgroup ------------------------------------------
-// Word r of thread tid: waves 1 .. NWAVE-1 hold the first (NT - 64) RREG words of the clip, wave 0
-// -- which runs the previous clip's endpoint scan while the others run R1 -- the rest (35 words of
-// a 1 s clip).
-__device__ __forceinline__ int pipe_word(int r, int tid)
-{
-    return tid >= 64 ? r * (NT - 64) + (tid - 64) : (NT - 64) * RREG + 64 * r + tid;
-}
-__device__ __forceinline__ void issue_clip_pipe(short8 (&regs)[NRV], const ExtractParams &p, const ClipRef &c, int tid)
-{
-#pragma unroll
-    for (int r = 0; r < RREG; r++) issue_word(&regs[4 * r], p, c, pipe_word(r, tid));
-}
-
-// The persistent loop keeps two clips in flight: B (the newer, whose words arrive in registers)
-// and A (the older, whose summaries are in LDS).  Each trip runs four barrier-separated stages:
-//   S1  wave 0: A's double-threshold scan;  waves 1-7 (+ wave 0 after it): B's R1 from registers
-//   S2  B's mean / peak, R2 (positive bits) and its pass-A partial-word loads; A's crop [st, en)
-//   S3  B's VAD frames (energies, ZCR);  A's windowed crop frames (R4)
-//   S4  the next clip's loads;  waves 0-5: A's 15 statistics (R5);  wave 6: B's p90;  wave 7: B's
-//       noise estimates
-// so the single-wave phases of one clip (scan, p90) run beside the multi-wave phases of the
-// other.  Per clip slot (A and B alternate between slots 0 and 1): the Shared record and the
-// positive bits; the word moments, VAD arrays and frame arrays are single (each is dead by the
-// time the other clip writes it).  A near tie leaves the clip DSP_CLIP_UNCERTIFIED for
-// extract_exact_kernel.
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVES_PER_EU))) void extract_pipe_kernel(ExtractParams p)
-{
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    constexpr ExtractCarve cv = extract_carve_fast();
-    const Ctx c0 = ctx_from(cv, lds);
-    Shared *const shs0 = c0.sh;
-    Shared *const shs1 = reinterpret_cast<Shared *>(lds + cv.sh2);
-    uint32_t *const posw0 = c0.posw;
-    uint32_t *const posw1 = reinterpret_cast<uint32_t *>(lds + cv.posw2);
-    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const int L = p.L, S = p.S;
-    WG_STAMP(16);
-    build_window(p, c0, (int)threadIdx.x, (int)threadIdx.x & 63, wid);
-    const int j0 = uni(shs0->j0), j1 = uni(shs0->j1);
-
-    const ClipQueue Q = queue_open(p, shs0);
-    if (threadIdx.x == 0) shs0->next = queue_next(Q, shs0);
-    __syncthreads();
-    int inext = uni(shs0->next);  // the clip whose words are in flight
-    ClipRef rnext = inext >= 0 ? clip_ref(p, inext) : clip_none();
-    short8 regs[NRV];
-    issue_clip_pipe(regs, p, rnext, (int)threadIdx.x);
-
-    int ia = -1, ib = -1, slotB = 1;
-    bool okA = false, okB = false;
-    ClipRef ra = clip_none(), rb = clip_none();
-    ClipStats sa{}, sb{};
-    for (;;) {
-        // rotate: B -> A, the in-flight clip -> B
-        ia = ib;
-        ra = rb;
-        sa = sb;
-        okA = okB;
-        ib = inext;
-        rb = rnext;
-        okB = ib >= 0 && rb.ok;
-        slotB ^= 1;
-        if (ia < 0 && ib < 0) break;
-        // the thread index, opaque to the optimiser once per trip: index arithmetic that depends
-        // only on it (word numbers, lane masks of the sorts) is then recomputed in the trip instead
-        // of being hoisted out of the loop and kept live (spilled) across it
-        int tid = (int)threadIdx.x;
-        asm volatile("" : "+v"(tid));
-        const int lane = tid & 63;
-        Shared *const shA = slotB ? shs0 : shs1, *const shB = slotB ? shs1 : shs0;
-        Ctx cA = c0, cB = c0;
-        cA.sh = shA;
-        cA.posw = slotB ? posw0 : posw1;
-        cB.sh = shB;
-        cB.posw = slotB ? posw1 : posw0;
-        // diagnostic stamps (make stamps), row of the trip's clip B: 0 trip start, 11 A's scan done,
-        // 1 S1 done, 2 S2 done, 12 / 14 S3 done on wave 7 / 0, 15 A's R5 (wave 0) done, 8 B's p90
-        // done (wave 6), 3 S4 done
-        STAMPW(ib, 0, 0);
-
-        // ---- S1 --------------------------------------------------------------------------------
-        if (tid == 0) shs0->next = ib >= 0 ? queue_next(Q, shs0) : -1;
-        if (wid == 0 && okA && sa.nv > 0) {
-            // the scan is the trip's single-wave critical path: issue priority over the
-            // co-resident workgroup's waves
-            __builtin_amdgcn_s_setprio(2);
-            const int flag = vad_scan<true, true>(p, cA, sa.nv, lane);
-            if (lane == 0) shA->exact = sa.Mp > 0.0 ? flag : 0;
-            __builtin_amdgcn_s_setprio(0);
-            STAMPW(ib, 11, 0);
-        }
-        if (okB) {
-            R1Acc acc = r1_acc_init();
-            const int nword = rb.nword;
-#pragma unroll
-            for (int r = 0; r < RREG; r++) {
-                const int w = pipe_word(r, tid);
-                if (w < nword) r1_word(&regs[4 * r], w, nword, rb.lead, rb.n, acc, c0.wS1, c0.wS2);
-            }
-            r1_reduce(acc, shB, wid, lane);
-        }
-        STAMPW(ib, 1, 0);
-        __syncthreads();  // B1
-
-        // ---- S2 --------------------------------------------------------------------------------
-        if (okB) sb = clip_stats(shB, rb.n, L, S, p.do_vad);
-        int st = 0, en = ra.n;
-        bool actA = okA;
-        if (okA && sa.nv > 0) {
-            if (uni(shA->exact)) {  // near tie: redone in numpy's exact order by extract_exact_kernel
-                actA = false;
-                if (tid == 0) p.status[ia] = DSP_CLIP_UNCERTIFIED;
-            } else {
-                if (uni(shA->n3) >= 0) {
-                    st = uni(shA->n1) * S;              // :272
-                    en = min(uni(shA->n6) * S + L, ra.n);  // :273
-                }
-                if (p.vad_energy)  // before S3 rewrites the VAD arrays
-                    for (int f = tid; f < sa.nv && f < p.ld_vad; f += NT) {
-                        p.vad_energy[(size_t)ia * p.ld_vad + f] = c0.vE[f];
-                        p.vad_zcr[(size_t)ia * p.ld_vad + f] = c0.vZ[f];
-                    }
-            }
-        }
-        if (ib >= 0 && !okB) write_bad_clip(p, ib, tid);  // empty or longer than the launch's cap
-        short8 qa[4];
-        int pa_w = -1, pa_e0 = 0, pa_e1 = 0;
-        if (okB) {
-            const int nword = rb.nword;
-#pragma unroll
-            for (int r = 0; r < RREG; r++) {
-                const int w = pipe_word(r, tid);
-                if (w < nword)
-                    cB.posw[w] = (DSP_ABL & 4) ? 0u : pos_word(&regs[4 * r], w, nword, rb.lead, rb.n, sb.tpos);
-            }
-            if (tid < 2) cB.posw[nword + tid] = 0;
-            // the partial words of pass A, in flight across the barrier
-            if (sb.nv > 0) pa_w = vad_partial_issue(p, rb, L, S, sb.nv, tid, qa, pa_e0, pa_e1);
-        }
-        inext = uni(shs0->next);
-        rnext = inext >= 0 ? clip_ref(p, inext) : clip_none();
-        STAMPW(ib, 2, 0);
-        __syncthreads();  // B2
-
-        // ---- S3 --------------------------------------------------------------------------------
-        // B's VAD frames (one lane pair per frame: waves 0-3) and A's crop frames (runs of two
-        // frames, four per wave: waves 7, 6, 5, 4 first) mostly run on different waves
-        if (okB && sb.nv > 0) vad_frames_fast(cB, rb, L, S, sb, qa, pa_w, pa_e0, pa_e1, tid);
-        int F = 0;
-        if (actA) F = r4_frames(p, cA, ra, st, en, sa, j0, j1, NWAVE - 1 - wid, lane);
-        STAMPW(ib, 12, NWAVE - 1);
-        STAMPW(ib, 14, 0);
-        __syncthreads();  // B3
-
-        // ---- S4 --------------------------------------------------------------------------------
-        // regs are dead since R2: the next clip's words load during S4 and S1 (unconditional, a
-        // clip_none() reads zeros, so the compiler's vmcnt bookkeeping stays exact)
-        issue_clip_pipe(regs, p, rnext, tid);
-        if (actA) {
-            r5_fast(c0, F, p.feat + (size_t)ia * 15, wid, lane);
-            if (p.seq)
-                for (int g = tid; g < F && g < p.ld_seq; g += NT) {
-                    float *o = p.seq + ((size_t)ia * p.ld_seq + g) * 3;
-                    o[0] = c0.fE[g];
-                    o[1] = c0.fM[g];
-                    o[2] = (float)c0.fZ[g];
-                }
-            if (tid == 0) {
-                p.start_end[2 * ia] = st;
-                p.start_end[2 * ia + 1] = en;
-                p.n_frames[ia] = F;
-                p.status[ia] = DSP_CLIP_OK;
-            }
-        }
-        STAMPW(ib, 15, 0);
-        if (okB && sb.nv > 0) {
-            if (wid == NWAVE - 2) {  // p90 order statistics (:198), then the scan: critical path
-                __builtin_amdgcn_s_setprio(2);
-                p90_select_wave(cB, sb.nv, lane);
-                __builtin_amdgcn_s_setprio(0);
-                STAMPW(ib, 8, NWAVE - 2);
-            } else if (wid == NWAVE - 1) {
-                vad_noise(cB, sb.nv, lane);
-            }
-        }
-        STAMPW(ib, 3, 0);
-        __syncthreads();  // B4
-    }
-    if (threadIdx.x == 0) queue_done(p);
-    WG_STAMP(22);
-}
-
-// ---- near ties: the endpoint energies in numpy's exact float64 order ----------------------------
-// Launched after extract_pipe_kernel / extract_kernel on the same stream: every clip they left
+// Launched after extract_kernel on the same stream: every clip they left
 // DSP_CLIP_UNCERTIFIED (rare) is redone from the start by one workgroup, on the bit-exact
 // (numpy-order) energy path, and gets its final outputs and DSP_CLIP_FLAG_VAD_EXACT.
 template <bool FAST>
@@ -1755,8 +1604,6 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return DSP_ERR_HIP;
         g_num_cus[dev] = prop.multiProcessorCount;
-        (void)hipFuncSetAttribute((const void *)dsp::extract_pipe_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
         (void)hipFuncSetAttribute((const void *)dsp::extract_kernel<true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, EXTRACT_LDS_LIMIT);
         (void)hipFuncSetAttribute((const void *)dsp::extract_kernel<false>,
@@ -1792,8 +1639,8 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     p.queue = (unsigned *)queue_ws;
     p.cv = extract_carve((int)max_len, frame_length, frame_shift);
     // persistent grid: two workgroups per CU when their LDS fits (one otherwise), each walking
-    // clip blockIdx first, then clips from the launch's queue; the compile-time layout (and the
-    // two-clip pipeline) whenever the launch fits it
+    // clip blockIdx first, then clips from the launch's queue; the compile-time layout whenever the
+    // launch fits it
     const bool fast = extract_fast_fits((int)max_len, frame_length, frame_shift);
     const size_t lds_launch = fast ? (size_t)extract_carve_fast().total : lds;
     const int per_cu = std::max(1, std::min<int>(EXTRACT_WG_PER_CU, (int)(EXTRACT_LDS_LIMIT / lds_launch)));
@@ -1801,11 +1648,7 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     const int grid = B < slots ? B : slots;
     const hipStream_t s = (hipStream_t)stream;
     if (fast) {
-#if EXTRACT_PIPE
-        hipLaunchKernelGGL(dsp::extract_pipe_kernel, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
-#else
         hipLaunchKernelGGL(dsp::extract_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
-#endif
         hipLaunchKernelGGL(dsp::extract_exact_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch + 4 * dsp::NT, s, p);
     } else {
         hipLaunchKernelGGL(dsp::extract_kernel<false>, dim3(grid), dim3(dsp::NT), lds_launch, s, p);

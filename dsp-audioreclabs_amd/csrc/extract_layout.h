@@ -19,22 +19,24 @@
 #endif
 #define EXTRACT_LDS_LIMIT (160 * 1024)   // one CU
 #define EXTRACT_SHARED_BYTES 512         // sizeof(dsp::Shared) rounded up (static_assert'ed)
-#define EXTRACT_WPAD 8                   // zero window entries on each side of the window table
-// (w, w^2) pairs per shifted window copy: copy r (0, 1) holds them for window index m - WPAD - r at
-// element m (zero outside [0, L)), so that the 8 pairs of a vector starting at any window index
-// are four aligned 16-B LDS reads from the copy of that index's parity
-#define EXTRACT_WROW(L) ((((L) + 2 * EXTRACT_WPAD + 4) + 3) & ~3)
+// Window table: per copy r (0, 1), pair slot P = {w_a, w_a+1, w2_a, w2_a+1} of window indices
+// a = 2P - WPAD - r (zero outside [0, L)), four slots (64 B) to a row and rows 80 B apart: the 8
+// (w, w^2) pairs of a vector starting at any window index are four aligned 16-B reads from the
+// copy of that index's parity, and the 64 lanes of a read (vectors 8 samples apart: rows one
+// apart) hit every LDS bank once per 16-lane group.  Rows 0-1 and the last two are zero.
+#define EXTRACT_WPAD 16
+#define EXTRACT_WRMAX(L) (((L) + 24) >> 3)                  // last clamp row (rows >= it are zero)
+#define EXTRACT_WCOPY(L) (80 * (EXTRACT_WRMAX(L) + 2))      // bytes per copy
 
 struct ExtractCarve {
-    int sh, wtab, posw, wS2, wS1, vE, vZ, fE, fM, fZ, rank, pS2, pS1, sh2, posw2, total;
+    int sh, wtab, posw, wS2, wS1, vE, vZ, fE, fM, fZ, rank, pS2, pS1, part, total;
     int nvcap, fcap, nwmax;
 };
 
 // Region offsets from the capacities: nwmax 32-sample words (incl. the alignment lead), nvcap VAD
-// frames, fcap feature frames, wrow floats per shifted window copy.  pipe: the second clip slot of
-// the pipelined FAST kernel (its Shared record and positive bits).
-__host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvcap, int fcap, int wrow,
-                                                              bool rank = true, bool pipe = false)
+// frames, fcap feature frames, wcopy bytes per window-table copy.
+__host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvcap, int fcap, int wcopy,
+                                                              bool rank = true)
 {
     ExtractCarve c{};
     int o = 0;
@@ -47,7 +49,7 @@ __host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvc
     c.fcap = fcap;
     c.nwmax = nwmax;
     DSP_TAKE(sh, EXTRACT_SHARED_BYTES);
-    DSP_TAKE(wtab, 16 * wrow);                   // 2 zero-padded copies of (w, w^2), shifted by 0..1
+    DSP_TAKE(wtab, 2 * wcopy);                   // 2 zero-padded copies of (w, w^2), shifted by 0..1
     DSP_TAKE(posw, 4 * (c.nwmax + 2));           // positive-sample bits (+2 zero sentinels)
     DSP_TAKE(wS2, 8 * c.nwmax);                  // per word: sum k^2 (exact, u64)
     DSP_TAKE(wS1, 4 * c.nwmax);                  // per word: sum k
@@ -59,8 +61,12 @@ __host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvc
     DSP_TAKE(rank, rank ? 4 * (c.nvcap > 3 * c.fcap ? c.nvcap : 3 * c.fcap) : 0);  // long clips only
     DSP_TAKE(pS2, 16 * c.nvcap);  // partial-word moments at the two ends of each VAD frame
     DSP_TAKE(pS1, 8 * c.nvcap);
-    DSP_TAKE(sh2, pipe ? EXTRACT_SHARED_BYTES : 0);
-    DSP_TAKE(posw2, pipe ? 4 * (c.nwmax + 2) : 0);
+    // R4 octet sums (8 x {E, M} per feature frame): over the word moments, dead after endpoint
+    // detection, when they fit
+    if (64 * c.fcap <= c.vE - c.wS2)
+        c.part = c.wS2;
+    else
+        DSP_TAKE(part, 64 * c.fcap);
 #undef DSP_TAKE
     c.total = o;
     return c;
@@ -72,28 +78,27 @@ __host__ __device__ inline ExtractCarve extract_carve(int ncap, int L, int S)
     const int nvcap = ncap >= L ? (ncap - L) / S + 1 : 0;
     const int fcap = ncap <= L ? 1 : (ncap - L + S - 1) / S + 1;
     const int nwmax = (ncap + 7 + 31) / 32 + 1;
-    return extract_carve_caps(nwmax, nvcap, fcap, EXTRACT_WROW(L));
+    return extract_carve_caps(nwmax, nvcap, fcap, EXTRACT_WCOPY(L));
 }
 
 // The fast kernel's layout is fixed at compile time (every LDS address an immediate) and serves
 // every launch whose clips fit it: the whole clip in registers, <= 128 VAD and feature frames,
-// window rows of <= EXTRACT_FAST_WROW floats (frame_length <= 1256).
+// frame_length <= EXTRACT_FAST_LMAX.
 #define EXTRACT_FAST_NV 128
 #define EXTRACT_FAST_NF 128
-#ifndef EXTRACT_FAST_WROW
-#define EXTRACT_FAST_WROW 1280
+#ifndef EXTRACT_FAST_LMAX
+#define EXTRACT_FAST_LMAX 1256
 #endif
 #define EXTRACT_FAST_NWORD (EXTRACT_THREADS * EXTRACT_RREG)
 __host__ __device__ constexpr ExtractCarve extract_carve_fast()
 {
-    return extract_carve_caps(EXTRACT_FAST_NWORD + 1, EXTRACT_FAST_NV, EXTRACT_FAST_NF, EXTRACT_FAST_WROW, false,
-                              true);
+    return extract_carve_caps(EXTRACT_FAST_NWORD + 1, EXTRACT_FAST_NV, EXTRACT_FAST_NF, EXTRACT_WCOPY(EXTRACT_FAST_LMAX), false);
 }
 __host__ __device__ inline bool extract_fast_fits(int ncap, int L, int S)
 {
     const ExtractCarve c = extract_carve(ncap, L, S);
     return (ncap + 7 + 31) / 32 <= EXTRACT_FAST_NWORD && c.nvcap <= EXTRACT_FAST_NV &&
-           c.fcap <= EXTRACT_FAST_NF && EXTRACT_WROW(L) <= EXTRACT_FAST_WROW;
+           c.fcap <= EXTRACT_FAST_NF && L <= EXTRACT_FAST_LMAX;
 }
 
 #endif
