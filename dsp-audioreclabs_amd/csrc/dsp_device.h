@@ -239,20 +239,12 @@ __device__ __forceinline__ double np_lerp(double a, double b, double g)
 // depend on where it sits in the packed buffer nor on which kernel ran it) ------------------------
 // A feature frame at clip sample fs with lim real samples (frame_signal :322-331) is summed over
 // the clip's 8-sample vectors v = va .. vb (va = fs >> 3, vb = (fs + lim - 1) >> 3; vector v =
-// clip samples 8v .. 8v + 7), CLIP-ABSOLUTE, in 64 lane classes: class l takes the vectors
-// v = l (mod 64) in increasing order, and each vector's pairs h = 0..3 in order, with
-// j = 8v + 2h (+1) - fs, w = (float)window[j] for 0 <= j < lim (else 0), w2 = fl(w * w),
+// clip samples 8v .. 8v + 7) by 16 lanes: lane l takes v = va + l + 16k in increasing k, and each
+// vector's pairs h = 0..3 in order, with j = 8v + 2h (+1) - fs, w = w_j for 0 <= j < lim (else 0),
 //   x = (float)k + xa            (near0: |round(mq)| <= 2; xa = fl(-mq), one rounding of k - mq)
 //   x = ((float)k + xa) + xb     (otherwise: xa = -t0, xb = -(mq - t0); k - t0 exact)
-//   e_t = fma(w2_t, fl(x_t * x_t), e_t),  m_t = fma(w_t, |x_t|, m_t)  (t = the pair's first / second,
-//   both from +0)
-// Class value c_l = e_0 + e_1 (m likewise); octet k (classes 8k .. 8k+7, r4_octet):
-//   o_k = ((c_8k + c_8k+1) + (c_8k+2 + c_8k+3)) + ((c_8k+4 + c_8k+5) + (c_8k+6 + c_8k+7))
-// and the frame's sum is o_0 + o_1 + ... + o_7 from the left (r4_sum8).  A vector outside the
-// frame adds +0 to a class value (w = 0, or x = 0 past the crop end), so a kernel may run a class
-// over more vectors than the frame's.  (The reference's windowed sample is y = w x, E = sum y^2,
-// M = sum |y|; the products are regrouped so that x^2 and |x| of a sample serve every frame that
-// holds it: fp32, within the 1e-5 tolerance.)
+//   y = w x,  e_t = fma(y_t, y_t, e_t),  m_t = m_t + |y_t|   (t = the pair's first / second sample)
+// Lane value (e_0 + e_1, m_0 + m_1); the frame's sum is dpp_row_reduce over the 16 lanes.
 struct CanonX {
     float xa, xb;
     bool near0;
@@ -281,47 +273,21 @@ __device__ __forceinline__ float2v canon_x2(int k0, int k1, const CanonX &c)
     const float2v a = {c.xa, c.xa}, b = {c.xb, c.xb};
     return NEAR0 ? k + a : (k + a) + b;
 }
-// w2 = fl(w * w) of a window weight (both kernels, one rounding)
-__device__ __forceinline__ float canon_w2(float w) { return w * w; }
-__device__ __forceinline__ float2v canon_w2(float2v w) { return w * w; }
-// the per-sample factors of a pair: q = fl(x * x), a = |x| (shared by every frame holding it)
-__device__ __forceinline__ void canon_qa(float2v x, float2v &q, float2v &a)
-{
-    q = x * x;
-    a = __builtin_elementwise_abs(x);
-}
 #pragma clang fp contract(on)
-// one pair into a frame's sums: e = fma(w2, q, e), m = fma(w, a, m) (v_pk_fma_f32, per component
-// exactly the scalar fma)
-__device__ __forceinline__ void canon_acc(float2v w, float2v w2, float2v q, float2v a, float2v &e, float2v &m)
+// one pair: weights w, x values x; y = w x (v_pk_mul_f32), e = fma(y, y, e) (v_pk_fma_f32),
+// m_t += |y_t| (v_add_f32 with the abs source modifier) -- per component exactly the scalar ops
+__device__ __forceinline__ float add_abs_f(float acc, float v)
 {
-    e = __builtin_elementwise_fma(w2, q, e);
-    m = __builtin_elementwise_fma(w, a, m);
+    float r;
+    asm("v_add_f32_e64 %0, |%1|, %2" : "=v"(r) : "v"(v), "v"(acc));
+    return r;
 }
-// the octet sums o_k of two sets of class values (lane l = class l; every lane of the octet gets
-// o_k, the same bits: each add is commutative): v_add_f32 with the DPP-permuted operand, one
-// instruction per stage, the two sets interleaved over the DPP read-after-write wait states
-// (every lane must be active)
-__device__ __forceinline__ void r4_octet2(float &e, float &m)
+__device__ __forceinline__ void canon_pair(float2v w, float2v x, float2v &e, float &m0, float &m1)
 {
-    asm volatile("s_nop 1\n\t"
-                 "v_add_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                 "v_add_f32_dpp %1, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                 "s_nop 0\n\t"
-                 "v_add_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-                 "v_add_f32_dpp %1, %1, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-                 "s_nop 0\n\t"
-                 "v_add_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
-                 "v_add_f32_dpp %1, %1, %1 row_half_mirror row_mask:0xf bank_mask:0xf"
-                 : "+v"(e), "+v"(m));
-}
-// o_0 + o_1 + ... + o_7, left to right
-__device__ __forceinline__ float r4_sum8(const float (&o)[8])
-{
-    float s = o[0];
-#pragma unroll
-    for (int k = 1; k < 8; k++) s += o[k];
-    return s;
+    const float2v y = w * x;
+    e = __builtin_elementwise_fma(y, y, e);
+    m0 = add_abs_f(m0, y.x);
+    m1 = add_abs_f(m1, y.y);
 }
 
 // acc + |v| in one VOP3 add with the abs source modifier

@@ -152,7 +152,7 @@ __device__ __forceinline__ ClipRef clip_none()
 
 struct Ctx {
     Shared *sh;
-    const float *wtab;  // window table: 2 copies of EXTRACT_WCOPY(L) bytes (extract_layout.h)
+    const float *wtab;  // EXTRACT_WROW(L) floats per shifted copy r = 0..3 (extract_layout.h)
     uint32_t *posw;      // bit u of the buffer: sample u is real and positive after preprocess
     unsigned long long *wS2;
     int *wS1;
@@ -163,7 +163,6 @@ struct Ctx {
     int *rank;  // rank scratch: nvcap or 3 * fcap ints
     int *pS1;   // partial-word moments at the two ends of each VAD frame (2 * nvcap)
     unsigned long long *pS2;
-    float2v *part;  // R4: the 8 octet sums {E, M} of each feature frame
     int64_t total;
     int stamp_clip;  // clip index for the diagnostic stamps
 };
@@ -728,198 +727,99 @@ __device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur
     }
 }
 
-// R4: windowed frames over the crop [st, en) (:378, :299-333; fe.py:12-43) -> c.fE / fM / fZ, in
-// the canonical order of dsp_device.h (lane l = class l).  The waves split the F frames into
-// contiguous ranges; a wave walks the 64-vector steps its frames cover (lane l: clip vector
-// 64 t + l, re-read from L2 by a 16-B load at the clip's own 2-byte alignment), turns each vector
-// into (x^2, |x|) once and adds it into every frame open in the step, up to R4_NSLOT at a time:
-// frame f0 + (s + R4_NSLOT j) G sits in slot s, G = r4_sweeps(L, S) sweeps (g: frames f0 + g + jG)
-// so that a slot's next frame never opens before its frame closes.  Per frame and sample pair
-// e = fma(w^2, x^2, e), m = fma(w, |x|, m); the 8 (w, w^2) pairs of a vector are four aligned 16-B
-// reads from the window table copy of the frame's parity (a vector wholly outside the window
-// reads a zero run: clamped element index).  A frame that closes is folded into its 8 octet sums
-// (c.part); after a barrier, four lanes per frame add them in order and count its sign changes.
-#define R4_NSLOT 4
-#ifndef R4_PF
-#define R4_PF 2  // 64-vector steps loaded ahead
+// R4: windowed frames over the crop [st, en) (:378, :299-333; fe.py:12-43) -> c.fE / fM / fZ.
+// One 16-lane row per frame (4 frames per wave), in the canonical order of dsp_device.h: the
+// frame's clip-relative 8-sample vectors are re-read from L2 (16-B loads at the clip's own 2-byte
+// alignment) and lane rl takes vectors va + rl + 16k, so the sums do not depend on where the clip
+// sits in the buffer and equal dsp_extract_general's.  Per sample y = w_j x (the reference's
+// windowed frame, :329-331), E += y^2, M += |y|; the weights of a vector's 8 samples are two
+// aligned 16-B reads from the window copy shifted by fs mod 4.  Returns F.
+#ifndef EXTRACT_R4_KV
+#define EXTRACT_R4_KV 9  // vectors per lane in one batch (a whole 1102-sample frame)
 #endif
-__host__ __device__ constexpr int r4_sweeps(int L, int S)
-{
-    // slot reuse: frame f + NSLOT G opens at least one step after frame f's last sample
-    return (L + 511 + R4_NSLOT * S - 1) / (R4_NSLOT * S);
-}
-__device__ __forceinline__ int med3_i(int x, int lo, int hi)
-{
-    int r;
-    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "s"(hi));
-    return r;
-}
-template <bool NEAR0>
-__device__ __forceinline__ void r4_sweep(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int st, int en,
-                                         int L, int S, int G, int f0, int fb, const CanonX &cx, int vfix,
-                                         short klast, int lane)
-{
-    const int flast = f0 + ((fb - 1 - f0) / G) * G;  // the sweep's frames f0, f0 + G, .. flast
-    const int ta = (st + f0 * S) >> 9, tb = (min(st + flast * S + L, en) - 1) >> 9;
-    const int wcopy = EXTRACT_WCOPY(L), rmax = EXTRACT_WRMAX(L);
-    const int n = cur.n;
-    // slot s: its frame fi (first sample fsm), the steps it opens and closes in, and where lane l's
-    // vector at step t starts in the window table: pair slot 4 (l + 64 t + U) + s0 of the copy at
-    // byte offset wb (rows 80 B apart, extract_layout.h)
-    int fi[R4_NSLOT], fsm[R4_NSLOT], topen[R4_NSLOT], tclose[R4_NSLOT], U[R4_NSLOT], s0[R4_NSLOT], wb[R4_NSLOT];
-    float2v e[R4_NSLOT], mm[R4_NSLOT];
-    auto derive = [&](int s) {  // from fi[s] and fsm[s]
-        const int r = fsm[s] & 1;
-        const bool in = fi[s] <= flast;
-        topen[s] = in ? fsm[s] >> 9 : 0x7fffffff;
-        tclose[s] = in ? (min(fsm[s] + L, en) - 1) >> 9 : -1;
-        const int c2 = (EXTRACT_WPAD + r - fsm[s]) >> 1;  // exact: WPAD + r - fsm is even
-        U[s] = c2 >> 2;
-        s0[s] = c2 & 3;
-        wb[s] = r ? wcopy : 0;
-    };
-    const int fstep = R4_NSLOT * G, sstep = R4_NSLOT * G * S;
-#pragma unroll
-    for (int s = 0; s < R4_NSLOT; s++) {
-        fi[s] = f0 + s * G;
-        fsm[s] = st + fi[s] * S;
-        derive(s);
-        e[s] = mm[s] = (float2v){0.f, 0.f};
-    }
-    const unsigned char *wt = reinterpret_cast<const unsigned char *>(c.wtab);
-    const int zero = 0;
-    auto step = [&](int t, const short8 &xv) {
-        const int v = 64 * t + lane;
-        float2v q[4], a[4];
-        if (512 * t + 512 >= en) {  // the crop's last step: samples from en on are frame_signal's zero padding
-            short8 k = xv;
-            if (vfix >= 0 && v == vfix) k[(n - 1) & 7] = klast;
-#pragma unroll
-            for (int h = 0; h < 4; h++) {
-                float2v x = canon_x2<NEAR0>(k[2 * h], k[2 * h + 1], cx);
-                const int u = 8 * v + 2 * h;
-                x.x = u < en ? x.x : 0.f;
-                x.y = u + 1 < en ? x.y : 0.f;
-                canon_qa(x, q[h], a[h]);
-            }
-        } else {
-#pragma unroll
-            for (int h = 0; h < 4; h++) canon_qa(canon_x2<NEAR0>(xv[2 * h], xv[2 * h + 1], cx), q[h], a[h]);
-        }
-#pragma unroll
-        for (int s = 0; s < R4_NSLOT; s++) {
-            if (t >= topen[s]) {  // open (a slot is reassigned when its frame closes)
-                // row clamped to the zero rows: a vector wholly outside the window reads zeros
-                const int R = med3_i(lane + (U[s] + 64 * t), zero, rmax);
-                const float4 *rp = reinterpret_cast<const float4 *>(wt + wb[s]) + 5 * R;  // 80-B rows
-                // pair h at slot s0 + h of the row (next row from slot 4 on: +16 B of row padding)
-                auto acc = [&](auto s0t) {
-                    constexpr int S0 = decltype(s0t)::value;
-#pragma unroll
-                    for (int h = 0; h < 4; h++) {
-                        const float4 ww = rp[S0 + h + (S0 + h >= 4 ? 1 : 0)];
-                        canon_acc((float2v){ww.x, ww.y}, (float2v){ww.z, ww.w}, q[h], a[h], e[s], mm[s]);
-                    }
-                    // a distinct marker per phase keeps the four variants apart (merged, their
-                    // immediate offsets would become per-dword address arithmetic)
-                    asm volatile("; r4 phase %0" ::"n"(S0));
-                };
-                switch (s0[s]) {
-                case 0: acc(IntT<0>()); break;
-                case 1: acc(IntT<1>()); break;
-                case 2: acc(IntT<2>()); break;
-                default: acc(IntT<3>()); break;
-                }
-            }
-        }
-#pragma unroll
-        for (int s = 0; s < R4_NSLOT; s++) {
-            if (t == tclose[s]) {
-                float eo = e[s].x + e[s].y, mo = mm[s].x + mm[s].y;
-                r4_octet2(eo, mo);
-                c.part[8 * fi[s] + (lane >> 3)] = (float2v){eo, mo};
-                e[s] = mm[s] = (float2v){0.f, 0.f};
-                fi[s] += fstep;
-                fsm[s] += sstep;
-                derive(s);
-            }
-        }
-    };
-    // R4_PF steps' vectors in flight
-    short8 xr[R4_PF];
-#pragma unroll
-    for (int k = 0; k < R4_PF; k++) xr[k] = load_cvec(p, cur, 64 * (ta + k) + lane);
-    for (int t = ta; t <= tb; t += R4_PF) {
-#pragma unroll
-        for (int k = 0; k < R4_PF; k++) {
-            if (k == 0 || t + k <= tb) {
-                step(t + k, xr[k]);
-                xr[k] = load_cvec(p, cur, 64 * (t + k + R4_PF) + lane);
-            }
-        }
-    }
-}
-
-// the frame sums in canonical order (octets 0..7 from the left) and the ZCR: four lanes per frame
-__device__ __forceinline__ void r4_finish(const Ctx &c, int st, int en, int L, int S, int F, int j0, int j1, int lead,
-                                          float sE, float sM, int tid)
-{
-    for (int b = 0; b < F; b += NT / 4) {
-        const int f = b + (tid >> 2), lq = tid & 3;
-        const bool act = f < F;
-        const int fs = st + (act ? f : 0) * S;
-        // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in [j0, j1])
-        // and before the crop end; transitions into the window's zero ends / padding count too
-        const int ia = fs + j0, ib = min(fs + j1, en - 1);  // sample coords
-        int z = dpp_quad_reduce((act && ia < ib) ? chg_count(c.posw, ia + lead, ib + lead, lq, 4) : 0, OpAdd());
-        if (act && lq == 0) {
-            if (ia <= ib) {
-                if (j0 > 0) z += pos_bit(c.posw, ia + lead);
-                if (ib < fs + L - 1) z += pos_bit(c.posw, ib + lead);
-            }
-            float oe[8], om[8];
-            const float4 *pp = reinterpret_cast<const float4 *>(c.part + 8 * f);
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const float4 u = pp[k];
-                oe[2 * k] = u.x;
-                om[2 * k] = u.y;
-                oe[2 * k + 1] = u.z;
-                om[2 * k + 1] = u.w;
-            }
-            c.fE[f] = r4_sum8(oe) * sE;
-            c.fM[f] = r4_sum8(om) * sM;
-            c.fZ[f] = z;
-        }
-    }
-}
-
-// Returns F.  Ends with a barrier.
 __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int st, int en,
-                                         const ClipStats &cs, int j0, int j1, int wrank, int tid)
+                                         const ClipStats &cs, int j0, int j1, int wrank, int lane)
 {
     const int L = p.L, S = p.S, n = cur.n, lead = cur.lead;
     const int m = en - st;  // > 0 always (start < end)
     const int F = (m <= L) ? 1 : (m - L + S - 1) / S + 1;
-    const int G = r4_sweeps(L, S);
+    const float sE = cs.invMf * cs.invMf, sM = cs.invMf;
+    const int wrow = EXTRACT_WROW(L);
     const CanonX cx = canon_x(cs.mq, cs.t0);
     // a 16-B load ending past the clip's last buffer vector drops a dword that straddles the
     // descriptor's end (range checks are per dword): with an odd lead and a clip ending on a
     // vector boundary that dword holds the last sample, patched in from the aligned vector
     const int vfix = ((lead & 1) && ((lead + n) & 7) == 0) ? (n - 1) >> 3 : -1;
     const short klast = vfix >= 0 ? load_vec(p, cur, cur.nvec - 1)[7] : (short)0;
-    const int lane = tid & 63;
-    const int fa = (F * wrank) / NWAVE, fb = (F * (wrank + 1)) / NWAVE;  // this wave's frames
-    if (!(DSP_ABL & 1))
-        for (int g = 0; g < G && fa + g < fb; g++) {
-            if (cx.near0)
-                r4_sweep<true>(p, c, cur, st, en, L, S, G, fa + g, fb, cx, vfix, klast, lane);
-            else
-                r4_sweep<false>(p, c, cur, st, en, L, S, G, fa + g, fb, cx, vfix, klast, lane);
+    auto frame_vec = [&](auto padded_t, auto near_t, const short8 &x8, const float *wr, int jb, int lim,
+                         float2v &ea, float &m0, float &m1) {
+        constexpr bool PADDED = decltype(padded_t)::value, NEAR0 = decltype(near_t)::value;
+        const float4 wa = *reinterpret_cast<const float4 *>(wr + jb);
+        const float4 wb = *reinterpret_cast<const float4 *>(wr + jb + 4);
+        const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            float2v w = {wv[2 * h], wv[2 * h + 1]};
+            if (PADDED) {  // samples past the crop are zero padding
+                const int j = jb + 2 * h;  // window index of the pair's first sample
+                w.x = j < lim ? w.x : 0.f;
+                w.y = j + 1 < lim ? w.y : 0.f;
+            }
+            canon_pair(w, canon_x2<NEAR0>(x8[2 * h], x8[2 * h + 1], cx), ea, m0, m1);
         }
-    __syncthreads();
-    const float sE = cs.invMf * cs.invMf, sM = cs.invMf;
-    r4_finish(c, st, en, L, S, F, j0, j1, lead, sE, sM, tid);
+    };
+    constexpr int KV = EXTRACT_R4_KV;
+    const int rl = lane & 15, row = lane >> 4;
+    for (int gi = wrank; !(DSP_ABL & 1) && 4 * gi < F; gi += NWAVE) {
+        const int g = 4 * gi + row;
+        const bool act = g < F;
+        const int gc = act ? g : F - 1;
+        const int fs = st + gc * S;
+        const int lim = min(L, en - fs);  // samples beyond the crop are zero padding
+        const bool padded = lim < L;
+        const int va = fs >> 3, vb = (fs + lim - 1) >> 3;
+        const int r = fs & 3;  // copy whose rows start at window index = -fs (mod 4)
+        const float *wr = c.wtab + r * wrow + EXTRACT_WPAD + r;  // wr[j] = w[j], j = -7 .. L + 7
+        float2v ea = {0.f, 0.f};
+        float m0 = 0.f, m1 = 0.f;
+        for (int v0 = va; v0 <= vb; v0 += 16 * KV) {
+            short8 xv[KV];
+#pragma unroll
+            for (int k = 0; k < KV; k++) xv[k] = load_cvec(p, cur, v0 + rl + 16 * k);
+            if (vfix >= 0)  // clip-uniform, rare
+#pragma unroll
+                for (int k = 0; k < KV; k++)
+                    if (v0 + rl + 16 * k == vfix) xv[k][(n - 1) & 7] = klast;
+            auto run = [&](auto pt, auto nt) {
+#pragma unroll
+                for (int k = 0; k < KV; k++) {
+                    const int v = v0 + rl + 16 * k;
+                    if (v <= vb) frame_vec(pt, nt, xv[k], wr, 8 * v - fs, lim, ea, m0, m1);
+                }
+            };
+            if (padded)
+                cx.near0 ? run(BoolT<true>(), BoolT<true>()) : run(BoolT<true>(), BoolT<false>());
+            else if (cx.near0)
+                run(BoolT<false>(), BoolT<true>());
+            else
+                run(BoolT<false>(), BoolT<false>());
+        }
+        const float E1 = dpp_row_reduce(ea.x + ea.y, OpAdd()) * sE;
+        const float M1 = dpp_row_reduce(m0 + m1, OpAdd()) * sM;
+        // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in
+        // [j0, j1]) and j < lim; transitions into the window's zero ends / padding count too
+        const int ia = fs + j0, ib = min(fs + j1, en - 1);  // sample coords
+        int z = dpp_row_reduce(ia < ib ? chg_count(c.posw, ia + lead, ib + lead, rl, 16) : 0, OpAdd());
+        if (ia <= ib) {
+            if (j0 > 0) z += pos_bit(c.posw, ia + lead);
+            if (ib < fs + L - 1) z += pos_bit(c.posw, ib + lead);
+        }
+        if (act && rl == 0) {
+            c.fE[g] = E1;
+            c.fM[g] = M1;
+            c.fZ[g] = z;
+        }
+    }
     return F;
 }
 
@@ -1287,7 +1187,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     STAMP(i, 4);
 
     // ---- R4: windowed frames over the crop [st, en) (r4_frames) --------------------------------
-    const int F = r4_frames(p, c, cur, st, en, cs, sh->j0, sh->j1, wid, tid);
+    const int F = r4_frames(p, c, cur, st, en, cs, sh->j0, sh->j1, wid, lane);
     STAMP(i, 12);
     if (!FAST && F > 128)
         for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
@@ -1399,7 +1299,6 @@ __device__ __forceinline__ Ctx ctx_from(const ExtractCarve &cv, unsigned char *l
     c.rank = reinterpret_cast<int *>(lds + cv.rank);
     c.pS1 = reinterpret_cast<int *>(lds + cv.pS1);
     c.pS2 = reinterpret_cast<unsigned long long *>(lds + cv.pS2);
-    c.part = reinterpret_cast<float2v *>(lds + cv.part);
     c.total = 0;
     c.stamp_clip = 0;
     return c;
@@ -1421,7 +1320,7 @@ __device__ __forceinline__ Ctx make_ctx(const ExtractParams &p, unsigned char *l
 // with a barrier.
 __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &c, int tid, int lane, int wid)
 {
-    unsigned char *wt = reinterpret_cast<unsigned char *>(const_cast<float *>(c.wtab));  // 2 copies
+    float *wt = const_cast<float *>(c.wtab);  // 4 copies of wrow floats
     Shared *sh = c.sh;
     const int L = p.L;
     constexpr int WPRE = 3;
@@ -1435,22 +1334,18 @@ __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &
         sh->j0 = L;
         sh->j1 = -1;
     }
-    const int wcopy = EXTRACT_WCOPY(L);
-    for (int t = tid; t < wcopy / 2; t += NT) reinterpret_cast<float *>(wt)[t] = 0.f;  // both copies
+    const int wrow = EXTRACT_WROW(L);
+    for (int t = tid; t < 4 * (wrow - L); t += NT) {  // zero pads: m < WPAD + r, m >= L + WPAD + r
+        const int r = t / (wrow - L), q = t - r * (wrow - L);
+        wt[r * wrow + (q < EXTRACT_WPAD + r ? q : q + L)] = 0.f;
+    }
     __syncthreads();
     auto put_weight = [&](int q0, double w) {  // weight j = q0 + lane (q0 wave-uniform)
         const int j = q0 + lane;
         const bool in = j < L;
         if (in) {
-            const float wf = (float)w;
 #pragma unroll
-            for (int r = 0; r < 2; r++) {
-                const int m = j + EXTRACT_WPAD + r;  // slot P = m >> 1, position m & 1
-                const int P = m >> 1;
-                float *slot = reinterpret_cast<float *>(wt + r * wcopy + 80 * (P >> 2) + 16 * (P & 3));
-                slot[m & 1] = wf;
-                slot[2 + (m & 1)] = canon_w2(wf);
-            }
+            for (int r = 0; r < 4; r++) wt[r * wrow + j + EXTRACT_WPAD + r] = (float)w;
         }
         const unsigned long long m = __ballot(in && w > 0.0);
         if (lane == 0 && m) {

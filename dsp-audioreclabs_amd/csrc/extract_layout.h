@@ -19,23 +19,19 @@
 #endif
 #define EXTRACT_LDS_LIMIT (160 * 1024)   // one CU
 #define EXTRACT_SHARED_BYTES 512         // sizeof(dsp::Shared) rounded up (static_assert'ed)
-// Window table: per copy r (0, 1), pair slot P = {w_a, w_a+1, w2_a, w2_a+1} of window indices
-// a = 2P - WPAD - r (zero outside [0, L)), four slots (64 B) to a row and rows 80 B apart: the 8
-// (w, w^2) pairs of a vector starting at any window index are four aligned 16-B reads from the
-// copy of that index's parity, and the 64 lanes of a read (vectors 8 samples apart: rows one
-// apart) hit every LDS bank once per 16-lane group.  Rows 0-1 and the last two are zero.
-#define EXTRACT_WPAD 16
-#define EXTRACT_WRMAX(L) (((L) + 24) >> 3)                  // last clamp row (rows >= it are zero)
-#define EXTRACT_WCOPY(L) (80 * (EXTRACT_WRMAX(L) + 2))      // bytes per copy
+#define EXTRACT_WPAD 8                   // zero window entries on each side of the window table
+// floats per shifted window copy: copy r holds w[m - WPAD - r] at m (zero outside [0, L)), so
+// that 4 consecutive weights starting at any window index are one aligned 16-B LDS read
+#define EXTRACT_WROW(L) ((((L) + 2 * EXTRACT_WPAD + 4) + 3) & ~3)
 
 struct ExtractCarve {
-    int sh, wtab, posw, wS2, wS1, vE, vZ, fE, fM, fZ, rank, pS2, pS1, part, total;
+    int sh, wtab, posw, wS2, wS1, vE, vZ, fE, fM, fZ, rank, pS2, pS1, total;
     int nvcap, fcap, nwmax;
 };
 
 // Region offsets from the capacities: nwmax 32-sample words (incl. the alignment lead), nvcap VAD
-// frames, fcap feature frames, wcopy bytes per window-table copy.
-__host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvcap, int fcap, int wcopy,
+// frames, fcap feature frames, wrow floats per shifted window copy.
+__host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvcap, int fcap, int wrow,
                                                               bool rank = true)
 {
     ExtractCarve c{};
@@ -49,7 +45,7 @@ __host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvc
     c.fcap = fcap;
     c.nwmax = nwmax;
     DSP_TAKE(sh, EXTRACT_SHARED_BYTES);
-    DSP_TAKE(wtab, 2 * wcopy);                   // 2 zero-padded copies of (w, w^2), shifted by 0..1
+    DSP_TAKE(wtab, 16 * wrow);                   // 4 zero-padded window copies, shifted by 0..3
     DSP_TAKE(posw, 4 * (c.nwmax + 2));           // positive-sample bits (+2 zero sentinels)
     DSP_TAKE(wS2, 8 * c.nwmax);                  // per word: sum k^2 (exact, u64)
     DSP_TAKE(wS1, 4 * c.nwmax);                  // per word: sum k
@@ -61,12 +57,6 @@ __host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvc
     DSP_TAKE(rank, rank ? 4 * (c.nvcap > 3 * c.fcap ? c.nvcap : 3 * c.fcap) : 0);  // long clips only
     DSP_TAKE(pS2, 16 * c.nvcap);  // partial-word moments at the two ends of each VAD frame
     DSP_TAKE(pS1, 8 * c.nvcap);
-    // R4 octet sums (8 x {E, M} per feature frame): over the word moments, dead after endpoint
-    // detection, when they fit
-    if (64 * c.fcap <= c.vE - c.wS2)
-        c.part = c.wS2;
-    else
-        DSP_TAKE(part, 64 * c.fcap);
 #undef DSP_TAKE
     c.total = o;
     return c;
@@ -78,27 +68,27 @@ __host__ __device__ inline ExtractCarve extract_carve(int ncap, int L, int S)
     const int nvcap = ncap >= L ? (ncap - L) / S + 1 : 0;
     const int fcap = ncap <= L ? 1 : (ncap - L + S - 1) / S + 1;
     const int nwmax = (ncap + 7 + 31) / 32 + 1;
-    return extract_carve_caps(nwmax, nvcap, fcap, EXTRACT_WCOPY(L));
+    return extract_carve_caps(nwmax, nvcap, fcap, EXTRACT_WROW(L));
 }
 
 // The fast kernel's layout is fixed at compile time (every LDS address an immediate) and serves
 // every launch whose clips fit it: the whole clip in registers, <= 128 VAD and feature frames,
-// frame_length <= EXTRACT_FAST_LMAX.
+// window rows of <= EXTRACT_FAST_WROW floats (frame_length <= 1256).
 #define EXTRACT_FAST_NV 128
 #define EXTRACT_FAST_NF 128
-#ifndef EXTRACT_FAST_LMAX
-#define EXTRACT_FAST_LMAX 1256
+#ifndef EXTRACT_FAST_WROW
+#define EXTRACT_FAST_WROW 1280
 #endif
 #define EXTRACT_FAST_NWORD (EXTRACT_THREADS * EXTRACT_RREG)
 __host__ __device__ constexpr ExtractCarve extract_carve_fast()
 {
-    return extract_carve_caps(EXTRACT_FAST_NWORD + 1, EXTRACT_FAST_NV, EXTRACT_FAST_NF, EXTRACT_WCOPY(EXTRACT_FAST_LMAX), false);
+    return extract_carve_caps(EXTRACT_FAST_NWORD + 1, EXTRACT_FAST_NV, EXTRACT_FAST_NF, EXTRACT_FAST_WROW, false);
 }
 __host__ __device__ inline bool extract_fast_fits(int ncap, int L, int S)
 {
     const ExtractCarve c = extract_carve(ncap, L, S);
     return (ncap + 7 + 31) / 32 <= EXTRACT_FAST_NWORD && c.nvcap <= EXTRACT_FAST_NV &&
-           c.fcap <= EXTRACT_FAST_NF && L <= EXTRACT_FAST_LMAX;
+           c.fcap <= EXTRACT_FAST_NF && EXTRACT_WROW(L) <= EXTRACT_FAST_WROW;
 }
 
 #endif

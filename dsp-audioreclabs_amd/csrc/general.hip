@@ -384,44 +384,40 @@ __device__ __forceinline__ void general_clip(const Params &p, Sh &s, const Ws &w
     }
 
     // ---- windowed frames of the crop [st, en) (:378, :299-333; fe.py:12-43) ---------------
-    // frame g covers crop samples [g S, g S + L), zero-padded past the crop.  One wave per frame,
-    // lane l = class l of the canonical order of dsp_device.h (the fused kernel's, same bits); the
+    // frame g covers crop samples [g S, g S + L), zero-padded past the crop.  One 16-lane row per
+    // frame, E / M in the canonical order of dsp_device.h (the fused kernel's, same bits); the
     // ZCR is exact either way.
     const CanonX cx = canon_x(mq, t0);
-    for (int64_t g = wid; g < F; g += NWAVE) {
-        const int64_t fs = st + g * S;
+    const int rl = lane & 15, row = lane >> 4;
+    for (int64_t gi = wid; 4 * gi < F; gi += NWAVE) {
+        const int64_t g = 4 * gi + row;
+        const bool act = g < F;
+        const int64_t fs = st + (act ? g : F - 1) * S;
         const int64_t lim = min((int64_t)L, en - fs);
         const int64_t va = fs >> 3, vb = (fs + lim - 1) >> 3;
-        float2v ea = {0.f, 0.f}, ma = {0.f, 0.f};
-        for (int64_t v = va + ((lane - va) & 63); v <= vb; v += 64)  // clip-absolute: v = lane (mod 64)
+        float2v ea = {0.f, 0.f};
+        float m0 = 0.f, m1 = 0.f;
+        for (int64_t v = va + rl; v <= vb; v += 16)
             for (int h = 0; h < 4; h++) {
-                float2v wv, xv, q, a;
+                float2v wv, xv;
                 for (int t = 0; t < 2; t++) {
                     const int64_t sj = 8 * v + 2 * h + t, j = sj - fs;
                     wv[t] = (j >= 0 && j < lim) ? (float)p.window[j] : 0.f;
                     xv[t] = sj < n ? canon_xval(sample(x, sj), cx) : 0.f;
                 }
-                canon_qa(xv, q, a);
-                canon_acc(wv, canon_w2(wv), q, a, ea, ma);
+                canon_pair(wv, xv, ea, m0, m1);
             }
-        float eo = ea.x + ea.y, mo = ma.x + ma.y;
-        r4_octet2(eo, mo);
-        float oe[8], om[8];
-        for (int k = 0; k < 8; k++) {
-            oe[k] = lane_read(eo, 8 * k);
-            om[k] = lane_read(mo, 8 * k);
-        }
+        const float es = dpp_row_reduce(ea.x + ea.y, OpAdd()), ms = dpp_row_reduce(m0 + m1, OpAdd());
         int zc = 0;
-        for (int j = lane; j + 1 < L; j += 64) {
+        for (int j = rl; j + 1 < L; j += 16) {
             const bool p0 = j < lim && p.window[j] > 0.0 && sample(x, fs + j) >= tpos;
             const bool p1 = j + 1 < lim && p.window[j + 1] > 0.0 && sample(x, fs + j + 1) >= tpos;
             zc += p0 != p1;
         }
         zc = dpp_row_reduce(zc, OpAdd());
-        zc = lane_read(zc, 0) + lane_read(zc, 16) + lane_read(zc, 32) + lane_read(zc, 48);
-        if (lane == 0) {
-            w.fE[g] = r4_sum8(oe) * (invMf * invMf);
-            w.fM[g] = r4_sum8(om) * invMf;
+        if (act && rl == 0) {
+            w.fE[g] = es * (invMf * invMf);
+            w.fM[g] = ms * invMf;
             w.fZ[g] = zc;
         }
     }
