@@ -43,6 +43,12 @@
 #define DSP_ABL 0 // 1 = R4 frames, 2 = R5 jobs, 4 = R2 sign bits, 8 = VAD pass-A partial moments
 #endif
 
+// 1: a clip's words are loaded while the previous clip's R5 runs (its registers live across R5);
+// 0: at the clip's start (the co-resident workgroups cover the wait)
+#ifndef EXTRACT_PREFETCH
+#define EXTRACT_PREFETCH 1
+#endif
+
 namespace dsp {
 
 static constexpr int NT = EXTRACT_THREADS;
@@ -982,7 +988,10 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     Shared *sh = c.sh;
     // (the generic layout's and the exact redo's index arithmetic spills when hoisted: opaque
     // thread index there)
-    const int tid = (FAST && !EXACT) ? (int)threadIdx.x : opaque_tid(), lane = tid & 63,
+#ifndef EXTRACT_OPAQUE_FAST
+#define EXTRACT_OPAQUE_FAST 0
+#endif
+    const int tid = (FAST && !EXACT && !EXTRACT_OPAQUE_FAST) ? (int)threadIdx.x : opaque_tid(), lane = tid & 63,
               wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
     // frame sizes opaque per clip as well: constants derived from them ((double)L, ...) are
     // recomputed in the clip instead of being kept live across the loop
@@ -1196,7 +1205,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     if constexpr (!EXACT)
         if (tid == 0) sh->next = resolve();  // claimed at the clip's start (-1: none)
     __syncthreads();
-    if constexpr (!EXACT) {
+    if constexpr (!EXACT && EXTRACT_PREFETCH) {
         // regs are dead since R2: the next clip's words load while R5 runs (unconditional, a
         // clip_none() reads zeros, so the compiler's vmcnt bookkeeping stays exact)
         const int nx = sh->next;
@@ -1408,7 +1417,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
                     sh->next = queue_end(Q, sh, cl);
                 }
             }
-            inflight = done;
+            inflight = EXTRACT_PREFETCH && done;
         }
         __syncthreads();  // LDS summaries are rewritten by the next clip; sh->next published
         i = sh->next;
