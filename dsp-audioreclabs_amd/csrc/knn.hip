@@ -764,7 +764,10 @@ static constexpr int KNN_DMAX = 4096;
 #define KNN_SEED_MIN_NR 32768
 #endif
 #ifndef KNN_SEED_WARM
-#define KNN_SEED_WARM 3072.0
+#define KNN_SEED_WARM 1024.0
+#endif
+#ifndef KNN_SEED_SAT
+#define KNN_SEED_SAT 16
 #endif
 
 int pick_kc(int k)
@@ -777,10 +780,13 @@ int pick_kc(int k)
 }
 
 // MFMA screen: reference splits.  Every workgroup of the grid is resident at once, so a CU's time
-// is (rows per split + a split's list warm-up W) x its waves, and a CU saturates at about two
-// waves per SIMD:  T(s) = (Nr / s + W) * max(waves on the busiest CU, 8).  W ~ 16k rows from a
-// threshold at +inf; far less from a seeded threshold.
-int pick_nsplit_mfma(int64_t Nr, int64_t Nq, int qpb, int cus, double warm = 16384.0)
+// is (rows per split + a split's list warm-up W) x its waves, and a CU saturates at `sat` waves:
+// T(s) = (Nr / s + W) * max(waves on the busiest CU, sat).  From a threshold at +inf, W ~ 16k rows
+// and two waves per SIMD saturate (sat 8); from a seeded threshold W ~ 1k rows, and a step then
+// inserts so rarely that the steps' dependency chains need four waves per SIMD to hide (sat 16):
+// 12.5k x 100k forced splits 4 / 6 / 8 / 10 / 12 / 16 / 20 measured 1.08 / 1.00 / 0.97 / 0.86 /
+// 0.87 / 0.91 / 0.88 ms (profiles/r04_knn_split_sweep.txt).
+int pick_nsplit_mfma(int64_t Nr, int64_t Nq, int qpb, int cus, double warm = 16384.0, int sat = 8)
 {
     const int64_t qblocks = (Nq + qpb - 1) / qpb;
     const int64_t maxs = std::max<int64_t>(1, std::min<int64_t>(64, (Nr + dsp::MQ_TR - 1) / dsp::MQ_TR));
@@ -788,7 +794,7 @@ int pick_nsplit_mfma(int64_t Nr, int64_t Nq, int qpb, int cus, double warm = 163
     double best_t = 1e300;
     for (int64_t s = 1; s <= maxs; s++) {
         const int64_t waves = (qblocks * s + cus - 1) / cus * dsp::MQ_W;
-        const double t = ((double)Nr / (double)s + warm) * (double)std::max<int64_t>(waves, 8);
+        const double t = ((double)Nr / (double)s + warm) * (double)std::max<int64_t>(waves, sat);
         if (t < best_t * (1.0 - 1e-9)) {
             best_t = t;
             best = (int)s;
@@ -858,7 +864,7 @@ KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
         if (atoi(e) == 0) l.rstride = l.nsample = 0;
 #endif
     l.nsplit = l.mfma ? pick_nsplit_mfma(Nr, Nq, dsp::mq_qpb(l.KC), device_cus(),
-                                         l.rstride ? KNN_SEED_WARM : 16384.0)
+                                         l.rstride ? KNN_SEED_WARM : 16384.0, l.rstride ? KNN_SEED_SAT : 8)
                       : pick_nsplit(Nr, Nq, l.hd ? dsp::KNN_TQ : dsp::KNN_TQ * dsp::KNN_QP);
 #ifdef DSP_KNN_DIAG  // diagnostic build only: forced split count (tools/knn_split_sweep.sh)
     if (const char *e = getenv("DSP_KNN_NSPLIT")) l.nsplit = std::max(1, std::min(64, atoi(e)));
