@@ -13,7 +13,7 @@ src, tag = sys.argv[1], sys.argv[2]
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def mean_counter(d, name, ks="extract_kernel"):
+def mean_counter(d, name, ks="dsp::extract_kernel<"):  # not extract_exact_kernel
     vals = collections.defaultdict(float)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
