@@ -538,10 +538,10 @@ __device__ __forceinline__ T kth_of(const T (&a)[KM], int k)  // a[k - 1], k run
     return v;
 }
 
-// One thread per query, lists of KM >= k entries (k <= 8: 8) held in registers; each split's KC
-// candidates are loaded together.
+// One thread per query (lists of KM = 32, k > 16: the group merge's networks at that length take
+// the compiler tens of minutes), each split's KC candidates loaded together.
 template <int KC, int KM>
-__global__ __launch_bounds__(64) void knn_merge(const double *__restrict__ ref, const double *__restrict__ query,
+__global__ __launch_bounds__(64) void knn_merge1(const double *__restrict__ ref, const double *__restrict__ query,
                           int64_t Nr, int64_t Nq, int D, int k, int nsplit, int64_t self_offset,
                           const float *__restrict__ cand_d, const int *__restrict__ cand_i,
                           const unsigned int *maxnorm_bits, double err_rel, double err_abs,
@@ -654,6 +654,195 @@ __global__ __launch_bounds__(64) void knn_merge(const double *__restrict__ ref, 
         pred[q] = best;
     }
 }
+
+// the KM smallest of two ascending lists (a: this lane's, the partner's via shuffle) into a,
+// ascending: elementwise min of a and the reversed partner list (a bitonic sequence holding the
+// KM smallest of the union), then a bitonic merge network
+template <int KM>
+__device__ __forceinline__ void merge_sorted_f(float (&a)[KM], int m)
+{
+    float b[KM];
+#pragma unroll
+    for (int i = 0; i < KM; i++) b[i] = __shfl_xor(a[i], m, 64);
+#pragma unroll
+    for (int i = 0; i < KM; i++) a[i] = fminf(a[i], b[KM - 1 - i]);
+#pragma unroll
+    for (int h = KM / 2; h > 0; h >>= 1)
+#pragma unroll
+        for (int i = 0; i < KM; i++)
+            if ((i & h) == 0) {
+                const float lo = fminf(a[i], a[i + h]), hi = fmaxf(a[i], a[i + h]);
+                a[i] = lo;
+                a[i + h] = hi;
+            }
+}
+// the same for (distance, index) pairs in cand_less order (a strict total order: the result is
+// the KM smallest pairs of the union whatever the lanes' shares were)
+template <int KM>
+__device__ __forceinline__ void merge_sorted_pairs(double (&dl)[KM], int (&il)[KM], int m)
+{
+    double bd[KM];
+    int bi[KM];
+#pragma unroll
+    for (int i = 0; i < KM; i++) {
+        bd[i] = __shfl_xor(dl[i], m, 64);
+        bi[i] = __shfl_xor(il[i], m, 64);
+    }
+#pragma unroll
+    for (int i = 0; i < KM; i++) {
+        const bool t = cand_less(bd[KM - 1 - i], bi[KM - 1 - i], dl[i], il[i]);
+        dl[i] = t ? bd[KM - 1 - i] : dl[i];
+        il[i] = t ? bi[KM - 1 - i] : il[i];
+    }
+#pragma unroll
+    for (int h = KM / 2; h > 0; h >>= 1)
+#pragma unroll
+        for (int i = 0; i < KM; i++)
+            if ((i & h) == 0) {
+                const bool t = cand_less(dl[i + h], il[i + h], dl[i], il[i]);
+                const double d0 = dl[i], d1 = dl[i + h];
+                const int i0 = il[i], i1 = il[i + h];
+                dl[i] = t ? d1 : d0;
+                il[i] = t ? i1 : i0;
+                dl[i + h] = t ? d0 : d1;
+                il[i + h] = t ? i0 : i1;
+            }
+}
+
+// MG lanes per query (8 queries per wave): lane j of a query's group takes the splits s = j
+// (mod MG), keeps its own fp32 k-th list (pass 1) and fp64 (distance, index) list (pass 2), and
+// the group merges them by a lane^1 / ^2 / ^4 butterfly.  The k-th smallest of a multiset and
+// the KM smallest (distance, index) pairs do not depend on how the candidates were shared, so
+// the results equal one thread walking every split (round 3's knn_merge); with MG times the
+// threads, a 12 500-query shard fills the chip instead of 196 waves.
+static constexpr int MG = 8;
+template <int KC, int KM>
+__global__ __launch_bounds__(64) void knn_merge(const double *__restrict__ ref, const double *__restrict__ query,
+                          int64_t Nr, int64_t Nq, int D, int k, int nsplit, int64_t self_offset,
+                          const float *__restrict__ cand_d, const int *__restrict__ cand_i,
+                          const unsigned int *maxnorm_bits, double err_rel, double err_abs,
+                          const int32_t *__restrict__ labels, int32_t *__restrict__ idx,
+                          double *__restrict__ dist, int32_t *__restrict__ pred, int *fb_count,
+                          int *fb_list, const float *__restrict__ seed)
+{
+    const int j = threadIdx.x % MG;
+    const int64_t qr = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / MG;
+    const bool live = qr < Nq;  // every lane takes part in the shuffles
+    const int64_t q = live ? qr : Nq - 1;
+    const double *qx = query + q * D;
+    double dl[KM];
+    int il[KM];
+#pragma unroll
+    for (int i = 0; i < KM; i++) {
+        dl[i] = INFINITY;
+        il[i] = 0x7fffffff;
+    }
+    double qn = 0.0;
+    for (int c = 0; c < D; c++) qn += qx[c] * qx[c];
+    // |fp32 screened distance - fp64 distance| <= err(d): fp32 rounding of the inputs and of the
+    // sum (direct or expanded form), coefficients from the host (knn_err_coeffs)
+    const double rmax = (double)__uint_as_float(*maxnorm_bits);
+    auto err = [&](double d) { return err_rel * d + err_abs * (qn + rmax) + 1e-30; };
+    const int64_t self = self_offset >= 0 ? self_offset + q : -1;
+    // pass 1 (fp32 only): the k-th smallest screened distance t32 and the screening cut-off of
+    // every split whose candidate list is full
+    float k32[KM];
+#pragma unroll
+    for (int i = 0; i < KM; i++) k32[i] = INFINITY;
+    // cut: every row the screen did not keep has a screened distance >= cut (a seeded screen keeps
+    // only rows below min(seed, the lists' thresholds))
+    float kth = INFINITY, cut = seed ? seed[q] : INFINITY;
+    for (int s = j; s < nsplit; s += MG) {
+        const size_t o = ((size_t)s * Nq + q) * KC;
+        int rr[KC];
+        float dd[KC];
+#pragma unroll
+        for (int i = 0; i < KC; i++) {
+            rr[i] = cand_i[o + i];
+            dd[i] = cand_d[o + i];
+        }
+#pragma unroll
+        for (int i = 0; i < KC; i++) {
+            // a value at or past this lane's k-th is not among the group's k smallest either
+            if (rr[i] < 0 || rr[i] == self || !(dd[i] < kth)) continue;
+            float v = dd[i];  // sorted insert into the KM smallest
+#pragma unroll
+            for (int jj = 0; jj < KM; jj++) {
+                const float lo = fminf(v, k32[jj]);
+                v = fmaxf(v, k32[jj]);
+                k32[jj] = lo;
+            }
+            kth = kth_of<KM>(k32, k);
+        }
+        if (rr[KC - 1] >= 0) cut = fminf(cut, dd[KC - 1]);
+    }
+#pragma unroll
+    for (int m = 1; m < MG; m <<= 1) {
+        merge_sorted_f<KM>(k32, m);
+        cut = fminf(cut, __shfl_xor(cut, m, 64));
+    }
+    kth = kth_of<KM>(k32, k);
+    // pass 2: fp64 re-rank (sklearn's own distance) of the candidates that can still be among the
+    // k nearest: a candidate with d - err(d) > t32 + err(t32) is farther (in fp64) than the k
+    // candidates at or below t32
+    const double t32 = (double)kth;
+    const double keep = t32 < INFINITY ? t32 + err(t32) : INFINITY;
+    for (int s = j; s < nsplit; s += MG) {
+        const size_t o = ((size_t)s * Nq + q) * KC;
+        int rr[KC];
+        float dd[KC];
+#pragma unroll
+        for (int i = 0; i < KC; i++) {
+            rr[i] = cand_i[o + i];
+            dd[i] = cand_d[o + i];
+        }
+#pragma unroll
+        for (int i = 0; i < KC; i++) {
+            const double d = (double)dd[i];
+            if (rr[i] < 0 || rr[i] == self || d - err(d) > keep) continue;
+            topk_fixed_insert<KM>(dl, il, rdist64(qx, ref + (int64_t)rr[i] * D, D), rr[i]);
+        }
+    }
+#pragma unroll
+    for (int m = 1; m < MG; m <<= 1) merge_sorted_pairs<KM>(dl, il, m);
+    if (!live || j != 0) return;
+    // certification: any row that was screened out has fp32 distance >= cut; its true fp64
+    // squared distance is >= cut - tol (fp32 rounding of inputs and of the sum).
+    const double tol = err((double)cut);
+    const bool ok = !(cut < INFINITY) || ((double)cut - tol > kth_of<KM>(dl, k));
+    if (!ok) {
+        const int slot = atomicAdd(fb_count, 1);
+        fb_list[slot] = (int)q;
+        return;
+    }
+    int outi[KM];
+#pragma unroll
+    for (int i = 0; i < KM; i++) {
+        const bool valid = dl[i] < INFINITY;
+        outi[i] = valid ? il[i] : -1;
+        if (i < k) {
+            idx[q * k + i] = outi[i];
+            dist[q * k + i] = valid ? sqrt(dl[i]) : INFINITY;
+        }
+    }
+    if (pred && labels) {  // scipy.stats.mode of the k labels: the smallest most frequent
+        int best = -1, bestc = 0;
+#pragma unroll
+        for (int a = 0; a < KM; a++) {
+            if (a >= k || outi[a] < 0) continue;
+            const int la = labels[outi[a]];
+            int cnt = 0;
+#pragma unroll
+            for (int b2 = 0; b2 < KM; b2++) cnt += b2 < k && outi[b2] >= 0 && labels[outi[b2]] == la;
+            if (cnt > bestc || (cnt == bestc && la < best)) {
+                bestc = cnt;
+                best = la;
+            }
+        }
+        pred[q] = best;
+    }
+}
+
 
 // exhaustive fp64 for the queries the screen could not certify: one workgroup per query
 static constexpr int FB_T = 256;
@@ -911,8 +1100,9 @@ bool launch_merge(hipStream_t s, const double *ref, const double *query, int64_t
                   double ea, const int32_t *lbl, int32_t *idx, double *dist, int32_t *pred, int *fbc, int *fbl,
                   const float *seed)
 {
-    // 64-thread workgroups: 12 500 queries (one rank of the 8-GPU self-query) are 196 of them
-    const dim3 g((unsigned)((Nq + 63) / 64)), b(64);
+    // 64-thread workgroups, MG lanes per query: 12 500 queries (one rank of the 8-GPU self-query)
+    // are 1 563 of them
+    const dim3 g((unsigned)((Nq * dsp::MG + 63) / 64)), b(64);
     // KC >= k + KNN_SLACK, so KC = 8 implies k <= 8 and KC = 16 implies k <= 16
     if (k > KC) return false;
     if (k <= 8) {
@@ -928,7 +1118,8 @@ bool launch_merge(hipStream_t s, const double *ref, const double *query, int64_t
         }
     }
     if constexpr (KC >= 24) {
-        hipLaunchKernelGGL((dsp::knn_merge<KC, 32>), g, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self, cd, ci,
+        const dim3 g1((unsigned)((Nq + 63) / 64));
+        hipLaunchKernelGGL((dsp::knn_merge1<KC, 32>), g1, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self, cd, ci,
                            mx, er, ea, lbl, idx, dist, pred, fbc, fbl, seed);
         return true;
     }
