@@ -57,7 +57,8 @@ def main():
     for _ in range(a.reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        idx, dist, pred = knn_classify(Xd, yd, Qd, a.k, self_offset=q0)
+        st = {}
+        idx, dist, pred = knn_classify(Xd, yd, Qd, a.k, self_offset=q0, stats=st)
         e1.record()
         torch.cuda.synchronize()
         times.append(e0.elapsed_time(e1) / 1e3)
@@ -65,6 +66,7 @@ def main():
     pairs = float(a.ref) * a.queries
     res = {"metric": "k-NN pairs/s (15-d, exact, KNeighborsClassifier semantics)",
            "value": round(pairs / t, 1), "unit": "pairs/s", "ms": round(t * 1e3, 4),
+           "fallbacks": st.get("fallbacks"),
            "config": {"ref": a.ref, "queries": a.queries, "dim": a.dim, "k": a.k, "self_query": True,
                       "data": "synthetic z-scored 15-d vectors around 10 class centres"},
            "roofline": {"bound": "mfma-f32", "achieved": round(pairs * FLOP_PER_PAIR / t / 1e12, 2),
