@@ -538,8 +538,8 @@ __device__ __forceinline__ T kth_of(const T (&a)[KM], int k)  // a[k - 1], k run
     return v;
 }
 
-// One thread per query (lists of KM = 32, k > 16: the group merge's networks at that length take
-// the compiler tens of minutes), each split's KC candidates loaded together.
+// One thread per query, each split's KC candidates loaded together: lists of KM = 16 / 32 (k > 8;
+// the group merge's networks at those lengths cost minutes of compile time per instantiation).
 template <int KC, int KM>
 __global__ __launch_bounds__(64) void knn_merge1(const double *__restrict__ ref, const double *__restrict__ query,
                           int64_t Nr, int64_t Nq, int D, int k, int nsplit, int64_t self_offset,
@@ -1110,15 +1110,15 @@ bool launch_merge(hipStream_t s, const double *ref, const double *query, int64_t
                            er, ea, lbl, idx, dist, pred, fbc, fbl, seed);
         return true;
     }
+    const dim3 g1((unsigned)((Nq + 63) / 64));  // one thread per query (k > 8)
     if constexpr (KC >= 16) {
         if (k <= 16) {
-            hipLaunchKernelGGL((dsp::knn_merge<KC, 16>), g, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self, cd, ci,
-                               mx, er, ea, lbl, idx, dist, pred, fbc, fbl, seed);
+            hipLaunchKernelGGL((dsp::knn_merge1<KC, 16>), g1, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self, cd,
+                               ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl, seed);
             return true;
         }
     }
     if constexpr (KC >= 24) {
-        const dim3 g1((unsigned)((Nq + 63) / 64));
         hipLaunchKernelGGL((dsp::knn_merge1<KC, 32>), g1, b, 0, s, ref, query, Nr, Nq, D, k, nsplit, self, cd, ci,
                            mx, er, ea, lbl, idx, dist, pred, fbc, fbl, seed);
         return true;
