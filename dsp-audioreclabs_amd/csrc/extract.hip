@@ -126,8 +126,11 @@ struct Shared {
     int qnext, qend, qcursor, qrange;  // clip queue (thread 0): the current chunk's next clip and end;
                                        // static split cursor; ranges used up
     int cdir, cy;                      // the pending claim (queue_begin / queue_end)
+    unsigned smask;                    // staged output slots (ost) ...
+    int schunk;                        // ... of this chunk
 };
 static_assert(sizeof(Shared) <= EXTRACT_SHARED_BYTES, "grow EXTRACT_SHARED_BYTES");
+static_assert((EXTRACT_OSTAGE & (EXTRACT_OSTAGE - 1)) == 0 && EXTRACT_OSTAGE <= 32, "chunk of 2^k <= 32 clips");
 
 struct ClipRef {
     int64_t base;  // 8-aligned first sample index of the clip's vectors
@@ -169,6 +172,9 @@ struct Ctx {
     int *rank;  // rank scratch: nvcap or 3 * fcap ints
     int *pS1;   // partial-word moments at the two ends of each VAD frame (2 * nvcap)
     unsigned long long *pS2;
+    float *ofeat;    // staged outputs of the clips of one chunk, slot = clip mod EXTRACT_OSTAGE:
+    int32_t *ose;    // feat [slot][15], start/end [slot][2], n_frames [slot], status [slot]
+    int32_t *onf, *ost;
     int64_t total;
     int stamp_clip;  // clip index for the diagnostic stamps
 };
@@ -886,7 +892,7 @@ __device__ __forceinline__ void r5_fast(const Ctx &c, int F, float *featb, int w
 // chunks (a static i, i + G, ... split ends on the slowest workgroup: 3.19-3.98 ms spread at
 // 100 000 clips).  p.queue == NULL: the static split.  Thread 0 only.
 #ifndef EXTRACT_CHUNK
-#define EXTRACT_CHUNK 4
+#define EXTRACT_CHUNK EXTRACT_OSTAGE
 #endif
 #ifndef EXTRACT_XCD_RANGES
 #define EXTRACT_XCD_RANGES 8  // 1: one range for every workgroup (A/B)
@@ -1000,7 +1006,10 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     asm volatile("" : "+s"(L), "+s"(S));
 #endif
     const int n = cur.n, lead = cur.lead, nword = cur.nword;
-    float *featb = p.feat + (size_t)i * 15;
+    // outputs: the main kernel stages them in LDS (slot i mod EXTRACT_OSTAGE) and the workgroup
+    // writes a chunk's clips together (flush_outputs); the exact redo writes them directly
+    const int oslot = i & (EXTRACT_OSTAGE - 1);
+    float *featb = EXACT ? p.feat + (size_t)i * 15 : c.ofeat + 15 * oslot;
     const int16_t *clip_g = p.pcm + cur.base + lead;  // the clip in global memory, sample coords
     STAMP(i, 0);
 #ifdef DSP_STAMPS
@@ -1272,10 +1281,21 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
             o[2] = (float)c.fZ[g];
         }
     if (tid == 0) {
-        p.start_end[2 * i] = st;
-        p.start_end[2 * i + 1] = en;
-        p.n_frames[i] = F;
-        p.status[i] = DSP_CLIP_OK | (EXACT ? DSP_CLIP_FLAG_VAD_EXACT : 0);
+        if constexpr (EXACT) {
+            p.start_end[2 * i] = st;
+            p.start_end[2 * i + 1] = en;
+            p.n_frames[i] = F;
+            p.status[i] = DSP_CLIP_OK | DSP_CLIP_FLAG_VAD_EXACT;
+        } else {
+            c.ose[2 * oslot] = st;
+            c.ose[2 * oslot + 1] = en;
+            c.onf[oslot] = F;
+            c.ost[oslot] = DSP_CLIP_OK;
+            const int ch = i / EXTRACT_OSTAGE;  // the staged slots belong to chunk sh->schunk
+            const unsigned m0 = sh->schunk == ch ? sh->smask : 0u;
+            sh->schunk = ch;
+            sh->smask = m0 | (1u << oslot);
+        }
     }
     STAMP(i, 6);
     return true;
@@ -1310,6 +1330,10 @@ __device__ __forceinline__ Ctx ctx_from(const ExtractCarve &cv, unsigned char *l
     c.rank = reinterpret_cast<int *>(lds + cv.rank);
     c.pS1 = reinterpret_cast<int *>(lds + cv.pS1);
     c.pS2 = reinterpret_cast<unsigned long long *>(lds + cv.pS2);
+    c.ofeat = reinterpret_cast<float *>(lds + cv.ost);
+    c.ose = reinterpret_cast<int32_t *>(lds + cv.ost + 4 * 15 * EXTRACT_OSTAGE);
+    c.onf = c.ose + 2 * EXTRACT_OSTAGE;
+    c.ost = c.onf + EXTRACT_OSTAGE;
     c.total = 0;
     c.stamp_clip = 0;
     return c;
@@ -1371,6 +1395,24 @@ __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &
 }
 
 
+// the staged outputs of the chunk holding clip `done` (slots in sh->smask) to global memory,
+// contiguous per array: one clip's 76 B written on its own reach HBM as ~190 B of partial
+// sectors once L2 has evicted the lines between neighbouring clips' writes
+__device__ __forceinline__ void flush_outputs(const ExtractParams &p, const Ctx &c, int done, int tid)
+{
+    constexpr int CH = EXTRACT_OSTAGE;
+    const int cb = done & ~(CH - 1);
+    // nothing staged for this chunk (its clips were deferred or bad: written directly) -> 0
+    const unsigned m = c.sh->schunk == cb / CH ? c.sh->smask : 0u;
+    for (int t = tid; t < 15 * CH; t += NT)
+        if ((m >> (t / 15)) & 1) p.feat[(size_t)cb * 15 + t] = c.ofeat[t];
+    if (tid < 2 * CH && ((m >> (tid >> 1)) & 1)) p.start_end[2 * (size_t)cb + tid] = c.ose[tid];
+    if (tid < CH && ((m >> tid) & 1)) {
+        p.n_frames[cb + tid] = c.onf[tid];
+        p.status[cb + tid] = c.ost[tid];
+    }
+}
+
 // FAST launches run extract_kernel<true>, one clip at a time per workgroup.  A two-clip pipeline
 // (the single-wave phases of one clip beside the multi-wave phases of the other, round 4) measured
 // 3.41 against 3.35 ms: the CU is bound by instruction issue and the pipeline added 10% VALU and
@@ -1394,7 +1436,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     WG_STAMP(16);
     build_window(p, c, tid, lane, wid);
     const ClipQueue Q = queue_open(p, sh);
-    if (tid == 0) sh->next = queue_next(Q, sh);
+    if (tid == 0) {
+        sh->next = queue_next(Q, sh);
+        sh->smask = 0;
+        sh->schunk = -1;
+    }
     __syncthreads();
     short8 regs[NRV];
     bool inflight = false;  // regs already hold clip i's loads (issued by the previous clip's R4)
@@ -1420,7 +1466,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
             inflight = EXTRACT_PREFETCH && done;
         }
         __syncthreads();  // LDS summaries are rewritten by the next clip; sh->next published
+        const int prev = i;
         i = sh->next;
+        if (i < 0 || (i ^ prev) >= EXTRACT_OSTAGE) flush_outputs(p, c, prev, tid);  // next clip in another chunk
     }
     if (tid == 0) queue_done(p);
     WG_STAMP(22);

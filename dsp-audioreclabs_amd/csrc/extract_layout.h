@@ -19,13 +19,16 @@
 #endif
 #define EXTRACT_LDS_LIMIT (160 * 1024)   // one CU
 #define EXTRACT_SHARED_BYTES 512         // sizeof(dsp::Shared) rounded up (static_assert'ed)
+#ifndef EXTRACT_OSTAGE
+#define EXTRACT_OSTAGE 4                 // clips per queue chunk, whose outputs are written together
+#endif
 #define EXTRACT_WPAD 8                   // zero window entries on each side of the window table
 // floats per shifted window copy: copy r holds w[m - WPAD - r] at m (zero outside [0, L)), so
 // that 4 consecutive weights starting at any window index are one aligned 16-B LDS read
 #define EXTRACT_WROW(L) ((((L) + 2 * EXTRACT_WPAD + 4) + 3) & ~3)
 
 struct ExtractCarve {
-    int sh, wtab, posw, wS2, wS1, vE, vZ, fE, fM, fZ, rank, pS2, pS1, total;
+    int sh, wtab, posw, wS2, wS1, vE, vZ, fE, fM, fZ, rank, pS2, pS1, ost, total;
     int nvcap, fcap, nwmax;
 };
 
@@ -57,6 +60,7 @@ __host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvc
     DSP_TAKE(rank, rank ? 4 * (c.nvcap > 3 * c.fcap ? c.nvcap : 3 * c.fcap) : 0);  // long clips only
     DSP_TAKE(pS2, 16 * c.nvcap);  // partial-word moments at the two ends of each VAD frame
     DSP_TAKE(pS1, 8 * c.nvcap);
+    DSP_TAKE(ost, 4 * 19 * EXTRACT_OSTAGE);  // staged outputs of one clip chunk (feat, start/end, frames, status)
 #undef DSP_TAKE
     c.total = o;
     return c;
