@@ -9,5 +9,5 @@ if [ "$2" != "skip-tests" ]; then
   tail -2 $O/gpu_tests.log
 fi
 if [ -x tools/ubench/misalign ]; then timeout -k 10 60 tools/ubench/misalign > $O/misalign.txt 2>&1; cat $O/misalign.txt; fi
-if [ -f dsp-audioreclabs_amd/lib/libdsp_audiorec_stamps.so ]; then bash tools/stamps_run.sh $T 100000 > /dev/null; cat gpurun_out/st_$T/report.txt | head -30; fi
+if [ -f dsp-audioreclabs_amd/lib/libdsp_audiorec_stamps.so ]; then bash tools/stamps_seq.sh $T stamps | head -30; fi
 bash tools/profile_round.sh $T
