@@ -104,9 +104,9 @@ struct ExtractParams {
     float *seq;
     int ld_seq;
     unsigned long long *stamps;  // diagnostic build only (else null)
-    unsigned *queue;             // caller's clip-queue counter pair (NULL: static split): [0] clips
-                                 // claimed past the first G, [1] workgroups done; both zero at
-                                 // launch, the last workgroup out zeroes them again
+    unsigned *queue;             // caller's clip-queue scratch (NULL: static split), zero at launch;
+                                 // the last workgroup out zeroes it again
+    int qchunk;                  // clips per queue chunk (host: 4, or 2 for short batches)
     ExtractCarve cv;             // LDS layout, computed on the host (kernel arguments can be
                                  // re-read instead of being held in registers)
 };
@@ -883,31 +883,31 @@ __device__ __forceinline__ void r5_fast(const Ctx &c, int F, float *featb, int w
 }
 
 // Clip queue (ABI 3).  p.queue: the caller's zeroed 64-byte scratch, words 0-7 the claim counters
-// of eight ranges of clip chunks (EXTRACT_CHUNK consecutive clips each; range x = the chunks
+// of eight ranges of clip chunks (p.qchunk consecutive clips each; range x = the chunks
 // [x nch / 8, (x + 1) nch / 8)), word 8 the count of workgroups done.  A workgroup claims chunks
 // from the range of the XCD it runs on (HW_REG_XCC_ID: placement is a performance matter only,
 // any id is correct), then from the others in turn once its own is exhausted: one atomic per chunk
 // instead of per clip, consecutive clips on one XCD -- their 76-B output rows share cache lines in
 // that XCD's L2 instead of leaving it as partial-line writes -- and fast workgroups take more
 // chunks (a static i, i + G, ... split ends on the slowest workgroup: 3.19-3.98 ms spread at
-// 100 000 clips).  p.queue == NULL: the static split.  Thread 0 only.
-#ifndef EXTRACT_CHUNK
-#define EXTRACT_CHUNK EXTRACT_OSTAGE
-#endif
+// 100 000 clips).  The chunk is 4 clips, 2 for batches of fewer than 64 clips per workgroup
+// (12 500 clips: 0.506 -> 0.484 ms, a shorter tail; 100 000: 3.387 against 3.409 ms with 2;
+// profiles/r04x_queue_chunk_ab.txt).  p.queue == NULL: the static split.  Thread 0 only.
 #ifndef EXTRACT_XCD_RANGES
 #define EXTRACT_XCD_RANGES 8  // 1: one range for every workgroup (A/B)
 #endif
 static_assert(EXTRACT_XCD_RANGES >= 1 && EXTRACT_XCD_RANGES <= 8, "queue_ws holds 8 range counters");
 struct ClipQueue {  // wave-uniform; the mutable state lives in Shared (thread 0 only)
     unsigned *q;
-    int B, nch, xcd;
+    int B, nch, xcd, ch;
 };
 __device__ __forceinline__ ClipQueue queue_open(const ExtractParams &p, Shared *sh)
 {
     ClipQueue Q;
     Q.q = p.queue;
     Q.B = p.B;
-    Q.nch = (p.B + EXTRACT_CHUNK - 1) / EXTRACT_CHUNK;
+    Q.ch = p.qchunk;  // a power of two <= EXTRACT_OSTAGE (host), so chunks never straddle a stage group
+    Q.nch = (p.B + Q.ch - 1) / Q.ch;
     Q.xcd = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;  // HW_REG_XCC_ID[3:0]
     if (threadIdx.x == 0) {
         sh->qnext = sh->qend = sh->qrange = 0;
@@ -952,9 +952,9 @@ __device__ __forceinline__ int queue_end(const ClipQueue &Q, Shared *sh, unsigne
     for (;;) {
         const unsigned c0 = (unsigned)(y * Q.nch / NR), c1 = (unsigned)((y + 1) * Q.nch / NR);
         if (c0 + ret < c1) {
-            const int first = (int)(c0 + ret) * EXTRACT_CHUNK;
+            const int first = (int)(c0 + ret) * Q.ch;
             sh->qnext = first + 1;
-            sh->qend = min(Q.B, first + EXTRACT_CHUNK);
+            sh->qend = min(Q.B, first + Q.ch);
             return first;
         }
         // this range is used up: the next one (a blocking claim, rare: the end of the launch)
@@ -1591,6 +1591,7 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     p.ld_seq = ld_seq;
     p.stamps = (unsigned long long *)g_stamp_buffer;
     p.queue = (unsigned *)queue_ws;
+    p.qchunk = 4;  // set below from the batch size
     p.cv = extract_carve((int)max_len, frame_length, frame_shift);
     // persistent grid: two workgroups per CU when their LDS fits (one otherwise), each walking
     // clip blockIdx first, then clips from the launch's queue; the compile-time layout whenever the
@@ -1600,6 +1601,8 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     const int per_cu = std::max(1, std::min<int>(EXTRACT_WG_PER_CU, (int)(EXTRACT_LDS_LIMIT / lds_launch)));
     const int slots = per_cu * num_cus;
     const int grid = B < slots ? B : slots;
+    p.qchunk = B < 64 * (int64_t)grid ? 2 : 4;  // short batches: a finer tail
+    static_assert(EXTRACT_OSTAGE >= 4, "qchunk <= EXTRACT_OSTAGE");
     const hipStream_t s = (hipStream_t)stream;
     if (fast) {
         hipLaunchKernelGGL(dsp::extract_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
