@@ -45,6 +45,9 @@
 
 // 1: a clip's words are loaded while the previous clip's R5 runs (its registers live across R5);
 // 0: at the clip's start (the co-resident workgroups cover the wait)
+#ifndef EXTRACT_STATS_W0
+#define EXTRACT_STATS_W0 1
+#endif
 #ifndef EXTRACT_PREFETCH
 #define EXTRACT_PREFETCH 1
 #endif
@@ -116,10 +119,16 @@ static_assert(__is_standard_layout(ExtractParams) && __is_trivially_copyable(Ext
 static_assert(sizeof(ExtractParams) <= 1024, "kernel argument block");
 
 // ------------------------------------------------------------------------------------------
+struct ClipStatsRaw {
+    double mq, Mp, invM2;
+    float invMf;
+    int tpos, t0, nv;
+};
 struct Shared {
     long long red_k[NWAVE];
     int red_a[NWAVE], red_b[NWAVE];
     double pa, pb;            // the two order statistics of the VAD energies around p90
+    ClipStatsRaw cs;          // EXTRACT_STATS_W0: the clip statistics, computed by wave 0
     double noise_e, noise_z;  // VAD noise estimates (:189-195, :239-245)
     double oslo[3], oshi[3];  // order statistics (F-1)/2 and F/2 of E, M, ZCR (medians)
     int n3, n1, n6, exact, j0, j1, next;
@@ -1041,7 +1050,25 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     }
     r1_reduce(acc, sh, wid, lane);
     __syncthreads();
+#if EXTRACT_STATS_W0
+    // wave 0 computes the clip statistics once and shares them (a second barrier), instead of
+    // every wave repeating the fp64 work
+    if (wid == 0) {
+        const ClipStats c0 = clip_stats(sh, n, L, S, p.do_vad);
+        if (lane == 0) sh->cs = {c0.mq, c0.Mp, c0.invM2, c0.invMf, c0.tpos, c0.t0, c0.nv};
+    }
+    __syncthreads();
+    ClipStats cs;
+    cs.mq = uni(sh->cs.mq);
+    cs.Mp = uni(sh->cs.Mp);
+    cs.invM2 = uni(sh->cs.invM2);
+    cs.invMf = uni(sh->cs.invMf);
+    cs.tpos = uni(sh->cs.tpos);
+    cs.t0 = uni(sh->cs.t0);
+    cs.nv = uni(sh->cs.nv);
+#else
     const ClipStats cs = clip_stats(sh, n, L, S, p.do_vad);
+#endif
     const double mq = cs.mq, Mp = cs.Mp;
     const int tpos = cs.tpos, t0 = cs.t0, nv = cs.nv;
     STAMP(i, 1);
