@@ -207,26 +207,31 @@ def main():
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed_x = time.perf_counter() - t0  # extraction only
     my_frames = float(sum(frames[i % P] for i in range(K)))
-    if world > 1:
-        t = torch.tensor([elapsed, my_frames, kern_ms], dtype=torch.float64, device=dev)
-        tmax = t.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t.clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        elapsed, total_frames, kern_ms = tmax[0].item(), tsum[1].item(), tmax[2].item()
-    else:
-        total_frames = my_frames
     del graph
 
-    # the exchange step before KNN (not part of the metric): one packed all-gather of every
-    # per-clip result (76 B/clip)
-    ag = None
+    # N > 1: configs[3] as BASELINE defines it -- every step is the rank's extraction followed by
+    # the exchange, ONE packed all-gather of every per-clip result (76 B/clip) over RCCL; launched
+    # from Python (the collective is not captured), K steps between barriers
+    elapsed_g, ag = None, None
     if world > 1:
+        def step(b):
+            out = fx(b)
+            return gather_packed({k: out[k] for k in ("feat", "start_end", "n_frames", "status")}, args.clips)
+        step(pool[0])
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(K):
+            step(pool[i % P])
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        elapsed_g = time.perf_counter() - t0
+        # the all-gather alone (median of 5), for the record
         out = fx(pool[0])
         res = {k: out[k] for k in ("feat", "start_end", "n_frames", "status")}
-        gather_packed(res, args.clips)
         torch.cuda.synchronize(dev)
         ts = []
         for _ in range(5):
@@ -238,6 +243,15 @@ def main():
         ag = {"ms": round(float(np.median(ts)) * 1e3, 4), "bytes": args.clips * OUT_BYTES_PER_CLIP,
               "collectives": 1, "backend": backend_name,
               "what": "feat/start_end/n_frames/status of all clips, packed, one %s all_gather" % backend_name}
+    if world > 1:
+        t = torch.tensor([elapsed_x, elapsed_g, my_frames, kern_ms], dtype=torch.float64, device=dev)
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        elapsed_x, elapsed_g, total_frames, kern_ms = tmax[0].item(), tmax[1].item(), tsum[2].item(), tmax[3].item()
+    else:
+        total_frames = my_frames
 
     sweep = window_sweep(args, fx, pool[0], dev, world, rank) if args.sweep_clips > 0 else None
     cfg0 = configs0_leg(args, pool[0], dev, world) if args.cfg0 else None
@@ -261,6 +275,7 @@ def main():
             if key in pm:
                 roof["traffic"] = pm[key]["hbm_bytes_per_launch"]
                 roof["traffic_source"] = pm[key]["source"]
+        elapsed = elapsed_g if elapsed_g is not None else elapsed_x
         result = {
             "metric": METRIC,
             "value": round(total_frames / elapsed, 1),
@@ -282,10 +297,17 @@ def main():
                        "clips": args.clips, "clips_per_gpu": C, "samples_per_clip": N, "frame_length": L,
                        "frame_shift": S, "window": args.window, "vad": vad, "input": "int16 PCM resident in HBM",
                        "frames_per_step": round(total_frames / K, 1),
-                       "parallelism": "dp%d (clips sharded, no collective in the step)" % world,
-                       "launch": "hip graph of the %d steps" % K if not args.no_graph else "python loop"},
+                       "parallelism": ("dp%d (clips sharded; each step = extraction + one packed %s all-gather "
+                                       "of the per-clip results)" % (world, backend_name)) if world > 1 else
+                                      "dp1 (no collective)",
+                       "launch": ("python loop of the %d steps (extraction + all-gather)" % K) if world > 1 else
+                                 ("hip graph of the %d steps" % K if not args.no_graph else "python loop")},
             "roofline": roof,
         }
+        if world > 1:
+            # the same K steps without the exchange (hip graph): what the kernel alone scales to
+            result["value_extract_only"] = round(total_frames / elapsed_x, 1)
+            result["ms_per_step_extract_only"] = round(elapsed_x / K * 1e3, 5)
         if rehearsal:
             result["rehearsal"] = True
             result["backend"] = backend_name
@@ -421,7 +443,7 @@ def knn_leg(args, dev, world, rank):
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        knn_sharded(knn_classify, Xd, yd, Xd, args.knn_k, self_query=True)
+        last = knn_sharded(knn_classify, Xd, yd, Xd, args.knn_k, self_query=True)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -436,8 +458,9 @@ def knn_leg(args, dev, world, rank):
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         # the C oracle (sklearn semantics, fp64) on a bounded sample of the same queries, timed on
-        # the host cores; the GPU's answers for those queries must equal it bit for bit
-        idx, dist_, pred = knn_sharded(knn_classify, Xd, yd, Xd, args.knn_k, self_query=True)
+        # the host cores; the answers of the last timed run for those queries must equal it bit
+        # for bit
+        idx, dist_, pred = last
         cpu = knn_cpu_baseline(X, y, args.knn_k, idx, dist_, pred)
     res = {"metric": "k-NN pairs/s (15-d, exact, k=%d, self-query, gathered)" % args.knn_k,
             "value": round(pairs / t, 1), "unit": "pairs/s", "ms": round(t * 1e3, 4),

@@ -474,6 +474,9 @@ __device__ __forceinline__ float lane_xor_f(float v, int m, int lane)
 template <int NH, typename K>
 __device__ __forceinline__ void wave_bitonic(K (&a)[NH], int lane)
 {
+    // the lane index opaque here: the per-stage lane masks are then computed where they are used
+    // instead of being hoisted out of a persistent loop and held (spilled) in SGPR pairs
+    asm volatile("" : "+v"(lane));
     constexpr int N = 64 * NH;
 #pragma unroll
     for (int size = 2; size <= N; size <<= 1) {

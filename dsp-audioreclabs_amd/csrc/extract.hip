@@ -135,8 +135,12 @@ struct Shared {
     int qnext, qend, qcursor, qrange;  // clip queue (thread 0): the current chunk's next clip and end;
                                        // static split cursor; ranges used up
     int cdir, cy;                      // the pending claim (queue_begin / queue_end)
+    long long nx_base;                 // clip_fast: the next clip's load range (clip_ref), read by
+    int nx_nvec;                       // thread 0 when it resolves the claim
     unsigned smask;                    // staged output slots (ost) ...
     int schunk;                        // ... of this chunk
+    int sclear;                        // the staged slots were flushed: thread 0 clears smask after
+                                       // the next barrier (flush_outputs reads it in every thread)
 };
 static_assert(sizeof(Shared) <= EXTRACT_SHARED_BYTES, "grow EXTRACT_SHARED_BYTES");
 static_assert((EXTRACT_OSTAGE & (EXTRACT_OSTAGE - 1)) == 0 && EXTRACT_OSTAGE <= 32, "chunk of 2^k <= 32 clips");
@@ -181,6 +185,8 @@ struct Ctx {
     int *rank;  // rank scratch: nvcap or 3 * fcap ints
     int *pS1;   // partial-word moments at the two ends of each VAD frame (2 * nvcap)
     unsigned long long *pS2;
+    short8 *slots;   // FAST: the 32-sample word of each partial VAD frame end t (4 vectors at slots[4t])
+    unsigned char *crop;  // FAST: crop buffer (clip sample s at byte 2 (s - sbase), sbase = 0 mod 8)
     float *ofeat;    // staged outputs of the clips of one chunk, slot = clip mod EXTRACT_OSTAGE:
     int32_t *ose;    // feat [slot][15], start/end [slot][2], n_frames [slot], status [slot]
     int32_t *onf, *ost;
@@ -215,17 +221,27 @@ __device__ __forceinline__ void issue_word(short8 *q, const ExtractParams &p, co
         q[k] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rs, 64 * w + 16 * k, 0, 0));
 }
 
-// the clip's first RREG words into registers (word r * NT + tid -> regs[4r .. 4r+3])
+// the clip's first RREG words into registers (word r * NT + tid -> regs[4r .. 4r+3]): one VGPR
+// offset (the thread's word) for all of them, the row in the scalar offset and the vector in the
+// immediate, so no vector instruction runs between the loads (a VGPR rewritten between them made
+// the compiler's vmcnt bookkeeping wait for the first loads to land)
 __device__ __forceinline__ void issue_clip(short8 (&regs)[NRV], const ExtractParams &p, const ClipRef &c,
                                            int tid = (int)threadIdx.x)
 {
+    const __amdgpu_buffer_rsrc_t rs = clip_rsrc(p, c);
+    const int voff = 64 * tid;
 #pragma unroll
-    for (int r = 0; r < RREG; r++) issue_word(&regs[4 * r], p, c, r * NT + tid);
+    for (int r = 0; r < RREG; r++)
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            regs[4 * r + k] = __builtin_bit_cast(
+                short8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16 * k, 64 * NT * r, 0));
 }
 // the thread index, opaque to the optimiser where it is taken: index arithmetic that depends
 // only on it is then recomputed there instead of being hoisted out of the persistent loop and kept
 // live (spilled) across it.  The FAST clip body takes it only in a cold path: taken once per clip
-// for the whole body it cost 9% (3.74 against 3.43 ms at 100 000 clips, profiles/r04o).
+// for the whole body it cost 9% in round 4's kernel (3.74 against 3.43 ms at 100 000 clips; DESIGN.md
+// section 9, the raw record was not kept).
 __device__ __forceinline__ int opaque_tid()
 {
     int t = (int)threadIdx.x;
@@ -487,9 +503,10 @@ __device__ __forceinline__ void partial_moments(const short8 (&q)[4], int e0, in
     const short2v ones = {1, 1};
     int s1 = 0;
     unsigned long long s2 = 0;
+    const short8 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];  // value selects (see r1_word)
 #pragma unroll 1
     for (int k = 0; k < 4; k++) {
-        const short8 v = k == 0 ? q[0] : k == 1 ? q[1] : k == 2 ? q[2] : q[3];
+        const short8 v = k == 0 ? q0 : k == 1 ? q1 : k == 2 ? q2 : q3;
         const uint32_t Mk = M >> (8 * k);
 #pragma unroll
         for (int h = 0; h < 4; h++) {  // pair 4k + h: elements 8k + 2h, 8k + 2h + 1
@@ -510,6 +527,11 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 __device__ __forceinline__ float uni(float v)
 {
     return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ long long uni_ll(long long v)
+{
+    const unsigned lo = __builtin_amdgcn_readfirstlane((int)v), hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+    return (long long)(((unsigned long long)hi << 32) | lo);
 }
 __device__ __forceinline__ double uni(double v)
 {
@@ -553,9 +575,12 @@ __device__ __forceinline__ void r1_word(const short8 *q, int w, int nword, int l
                 s2 += (unsigned)sq2(d);  // <= 2^31: unsigned
             }
     } else {  // first / last word of the clip: real samples only
+        // select among values (v_cndmask), never among pointers into the caller's register array:
+        // a pointer select in a rolled loop moves the whole array to scratch
+        const short8 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
 #pragma unroll 1
         for (int k = 0; k < 4; k++) {
-            const short8 v = k == 0 ? q[0] : k == 1 ? q[1] : k == 2 ? q[2] : q[3];
+            const short8 v = k == 0 ? q0 : k == 1 ? q1 : k == 2 ? q2 : q3;
 #pragma unroll
             for (int e = 0; e < 8; e++) {
                 const int u = 32 * w + 8 * k + e;
@@ -748,29 +773,41 @@ __device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur
 }
 
 // R4: windowed frames over the crop [st, en) (:378, :299-333; fe.py:12-43) -> c.fE / fM / fZ.
-// One 16-lane row per frame (4 frames per wave), in the canonical order of dsp_device.h: the
-// frame's clip-relative 8-sample vectors are re-read from L2 (16-B loads at the clip's own 2-byte
-// alignment) and lane rl takes vectors va + rl + 16k, so the sums do not depend on where the clip
-// sits in the buffer and equal dsp_extract_general's.  Per sample y = w_j x (the reference's
-// windowed frame, :329-331), E += y^2, M += |y|; the weights of a vector's 8 samples are two
-// aligned 16-B reads from the window copy shifted by fs mod 4.  Returns F.
+// One 16-lane row per frame (4 frames per wave), in the canonical order of dsp_device.h: lane rl
+// takes the frame's clip-relative 8-sample vectors va + rl + 16k, so the sums do not depend on
+// where the clip sits in the buffer and equal dsp_extract_general's.  The vectors come from the
+// LDS crop buffer (FROM_LDS: 16-B aligned there, vector v at crop vector v - sb8) or are re-read from
+// L2 (16-B loads at the clip's own 2-byte alignment).  Per sample y = w_j x (the reference's windowed
+// frame, :329-331), E += y^2, M += |y|; the weights of a vector's 8 samples are two aligned 16-B
+// reads from the window copy shifted by fs mod 4.  Returns F.
 #ifndef EXTRACT_R4_KV
-#define EXTRACT_R4_KV 9  // vectors per lane in one batch (a whole 1102-sample frame)
+#define EXTRACT_R4_KV 9  // vectors per lane in one batch from L2 (a whole 1102-sample frame)
 #endif
-__device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int st, int en,
-                                         const ClipStats &cs, int j0, int j1, int wrank, int lane)
+#ifndef EXTRACT_R4L_KV
+#define EXTRACT_R4L_KV 4  // the same from the LDS crop buffer (the next clip's loads are in flight)
+#endif
+#ifndef EXTRACT_R4F_KV
+#define EXTRACT_R4F_KV 5  // clip_fast's L2 fallback (a crop larger than the LDS buffer)
+#endif
+template <bool FROM_LDS, int KV = FROM_LDS ? EXTRACT_R4L_KV : EXTRACT_R4_KV>
+__device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int L, int S,
+                                         int st, int en, const ClipStats &cs, int j0, int j1, int sb8, int wrank,
+                                         int lane, int vfix_lds = -1, short klast_lds = 0)
 {
-    const int L = p.L, S = p.S, n = cur.n, lead = cur.lead;
+    const int n = cur.n, lead = cur.lead;
     const int m = en - st;  // > 0 always (start < end)
     const int F = (m <= L) ? 1 : (m - L + S - 1) / S + 1;
     const float sE = cs.invMf * cs.invMf, sM = cs.invMf;
     const int wrow = EXTRACT_WROW(L);
     const CanonX cx = canon_x(cs.mq, cs.t0);
-    // a 16-B load ending past the clip's last buffer vector drops a dword that straddles the
+    // (L2) a 16-B load ending past the clip's last buffer vector drops a dword that straddles the
     // descriptor's end (range checks are per dword): with an odd lead and a clip ending on a
     // vector boundary that dword holds the last sample, patched in from the aligned vector
-    const int vfix = ((lead & 1) && ((lead + n) & 7) == 0) ? (n - 1) >> 3 : -1;
-    const short klast = vfix >= 0 ? load_vec(p, cur, cur.nvec - 1)[7] : (short)0;
+    // (LDS) the caller's: the crop DMA reads through the same descriptor, and the patch value is
+    // loaded before the next clip's loads are issued (a load here would wait for them)
+    const int vfix = FROM_LDS ? vfix_lds : ((lead & 1) && ((lead + n) & 7) == 0) ? (n - 1) >> 3 : -1;
+    const short klast = FROM_LDS ? klast_lds : vfix >= 0 ? load_vec(p, cur, cur.nvec - 1)[7] : (short)0;
+    const short8 *crop16 = reinterpret_cast<const short8 *>(c.crop);
     auto frame_vec = [&](auto padded_t, auto near_t, const short8 &x8, const float *wr, int jb, int lim,
                          float2v &ea, float &m0, float &m1) {
         constexpr bool PADDED = decltype(padded_t)::value, NEAR0 = decltype(near_t)::value;
@@ -788,7 +825,6 @@ __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, c
             canon_pair(w, canon_x2<NEAR0>(x8[2 * h], x8[2 * h + 1], cx), ea, m0, m1);
         }
     };
-    constexpr int KV = EXTRACT_R4_KV;
     const int rl = lane & 15, row = lane >> 4;
     for (int gi = wrank; !(DSP_ABL & 1) && 4 * gi < F; gi += NWAVE) {
         const int g = 4 * gi + row;
@@ -803,19 +839,27 @@ __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, c
         float2v ea = {0.f, 0.f};
         float m0 = 0.f, m1 = 0.f;
         for (int v0 = va; v0 <= vb; v0 += 16 * KV) {
+            // the lane's vectors v0 + rl + 16k: one per-lane base (vl) and immediate offsets, a
+            // per-lane bound (vlim) against uniform 16k -- nine hoisted per-k indices spilled at
+            // 80 VGPRs and every reload waited for all of the batch's loads
+            const int vl = v0 + rl, vlim = vb - vl;
             short8 xv[KV];
 #pragma unroll
-            for (int k = 0; k < KV; k++) xv[k] = load_cvec(p, cur, v0 + rl + 16 * k);
+            for (int k = 0; k < KV; k++) {
+                if constexpr (FROM_LDS)
+                    xv[k] = crop16[min(vl + 16 * k, vb) - sb8];
+                else
+                    xv[k] = load_cvec(p, cur, vl + 16 * k);
+            }
             if (vfix >= 0)  // clip-uniform, rare
 #pragma unroll
                 for (int k = 0; k < KV; k++)
-                    if (v0 + rl + 16 * k == vfix) xv[k][(n - 1) & 7] = klast;
+                    if (vl + 16 * k == vfix) xv[k][(n - 1) & 7] = klast;
+            const int jl = 8 * vl - fs;  // window index of the lane's first vector
             auto run = [&](auto pt, auto nt) {
 #pragma unroll
-                for (int k = 0; k < KV; k++) {
-                    const int v = v0 + rl + 16 * k;
-                    if (v <= vb) frame_vec(pt, nt, xv[k], wr, 8 * v - fs, lim, ea, m0, m1);
-                }
+                for (int k = 0; k < KV; k++)
+                    if (16 * k <= vlim) frame_vec(pt, nt, xv[k], wr, jl + 128 * k, lim, ea, m0, m1);
             };
             if (padded)
                 cx.near0 ? run(BoolT<true>(), BoolT<true>()) : run(BoolT<true>(), BoolT<false>());
@@ -1050,6 +1094,11 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     }
     r1_reduce(acc, sh, wid, lane);
     __syncthreads();
+    if (!EXACT && tid == 0 && sh->sclear) {  // the last flush's slots (every thread has read them)
+        sh->smask = 0;
+        sh->schunk = -1;
+        sh->sclear = 0;
+    }
 #if EXTRACT_STATS_W0
     // wave 0 computes the clip statistics once and shares them (a second barrier), instead of
     // every wave repeating the fp64 work
@@ -1234,7 +1283,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     STAMP(i, 4);
 
     // ---- R4: windowed frames over the crop [st, en) (r4_frames) --------------------------------
-    const int F = r4_frames(p, c, cur, st, en, cs, sh->j0, sh->j1, wid, lane);
+    const int F = r4_frames<false>(p, c, cur, L, S, st, en, cs, sh->j0, sh->j1, 0, wid, lane);
     STAMP(i, 12);
     if (!FAST && F > 128)
         for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
@@ -1328,6 +1377,374 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     return true;
 }
 
+// ==== FAST launches: clip_fast =================================================================
+// The clip's words stay in registers from R1 until the endpoint decisions are made; nothing of the
+// clip is re-read from memory:
+//   R1  registers: exact moments per word + sum / min / max; every word that holds a VAD frame
+//       end strictly inside it is also stored to that end's LDS slot (pass A reads it there)
+//   R2  registers: positive-sample bits
+//   VAD frames (LDS), p90 (wave 0) + noise (wave 1), scan (wave 0); thread 0 resolves the next clip
+//   crop: the words covering [st, en) are copied from the registers into the LDS crop buffer at the
+//       clip's own alignment; the registers are then dead and take the next clip's loads, in
+//       flight through R4, R5 and the loop turn
+//   R4  windowed crop frames from LDS;  R5 statistics
+// A crop larger than the buffer (no speech found, VAD off) takes R4 from L2, then the next loads.
+
+#ifndef EXTRACT_FAST_PREFETCH
+#define EXTRACT_FAST_PREFETCH 1  // 0: each clip's loads are issued at its start (3 workgroups per CU)
+#endif
+#ifndef EXTRACT_CROP_DMA
+#define EXTRACT_CROP_DMA 1  // the crop into LDS by LDS-DMA from L2 (0: copied from the registers)
+#endif
+// floor(a / S) and a mod S (S >= 1, |a| < 2^20) by the float reciprocal and one correction step
+__device__ __forceinline__ int div_floor(int a, int S, float invS, int &m)
+{
+    int q = (int)floorf((float)a * invS);
+    m = a - q * S;
+    if (m >= S) {
+        m -= S;
+        q++;
+    } else if (m < 0) {
+        m += S;
+        q--;
+    }
+    return q;
+}
+// The VAD frame ends strictly inside buffer word w (S >= 32 and L >= 64: at most one frame start and
+// one frame end, never both ends of one frame): ts = 2f for the start of frame f, te = 2f + 1 for
+// its end (-1: none) -- exactly the frame ends vad_partial_word maps to word w.
+__device__ __forceinline__ void word_frame_ends(int w, int lead, int L, int S, float invS, int nv, int &ts, int &te)
+{
+    const int a = 32 * w - lead;  // clip sample of the word's first buffer sample (>= -7)
+    int m;
+    const int fs = div_floor(a, S, invS, m) + 1;  // the first frame start > a is fs S = a + S - m
+    ts = (m > S - 32 && fs < nv) ? 2 * fs : -1;
+    const int fe = div_floor(a - L, S, invS, m) + 1;  // the first frame end > a: fe S + L
+    te = (m > S - 32 && fe >= 0 && fe < nv) ? 2 * fe + 1 : -1;
+}
+__device__ __forceinline__ void store_slot(short8 *slots, int t, const short8 *q)
+{
+#pragma unroll
+    for (int k = 0; k < 4; k++) slots[4 * t + k] = q[k];
+}
+
+// VAD frames, FAST layout (nv <= 128 <= NT / 2): one lane pair per frame -- lane h of pair f owns
+// frame end t = 2f + h = tid and adds the exact moments of its partial word (from its LDS slot),
+// plus half of the interior word sums and of the sign changes.  Frame f = buffer samples [u0, u0 + L):
+// exact moments (wS1/wS2 words + the partial words at its ends), sign changes from the positive
+// bits -> c.vE / c.vZ.
+__device__ __forceinline__ void vad_frames_slots(const Ctx &c, const ClipRef &cur, int L, int S, const ClipStats &cs,
+                                                 int tid)
+{
+    const int nv = cs.nv, lead = cur.lead;
+    const int f = tid >> 1, lh = tid & 1;
+    const bool act = f < nv;
+    int s1 = 0;
+    unsigned long long s2 = 0;
+    int zc = 0;
+    if (act) {
+        int e0, e1;
+        const int pw = vad_partial_word(cur, L, S, nv, tid, e0, e1);
+        if (pw >= 0 && !(DSP_ABL & 8)) {
+            short8 qa[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) qa[k] = c.slots[4 * tid + k];
+            partial_moments(qa, e0, e1, s1, s2);
+        }
+        const int u0 = lead + f * S, u1 = u0 + L;
+        const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
+        const int wi0 = (u0 & 31) ? wa + 1 : wa, wi1 = (u1 & 31) ? wb - 1 : wb;
+        const int per = (wi1 - wi0 + 2) >> 1;
+        const int ws = wi0 + lh * per, we = min(ws + per - 1, wi1);
+#pragma unroll 4
+        for (int w = ws; w <= we; w++) {
+            s1 += c.wS1[w];
+            s2 += c.wS2[w];
+        }
+        const int np_ = L - 1, ph = (np_ + 1) >> 1;  // pairs [u0, u1 - 1) in halves
+        const int x0 = u0 + min(lh * ph, np_), x1 = u0 + min((lh + 1) * ph, np_);
+        zc = chg_run(c.posw, x0, x1);
+    }
+    s1 += dpp_i(s1, DPP_QXOR1);
+    {
+        const unsigned lo = dpp_i((int)(unsigned)s2, DPP_QXOR1), hi = dpp_i((int)(unsigned)(s2 >> 32), DPP_QXOR1);
+        s2 += ((unsigned long long)hi << 32) | lo;
+    }
+    zc += dpp_i(zc, DPP_QXOR1);
+    if (act && lh == 0) {
+        c.vE[f] = energy_from_moments(s2, s1, L, cs.t0, cs.mq - (double)cs.t0, cs.invM2);
+        c.vZ[f] = zc;
+    }
+}
+
+// one buffer word (32 samples, 16 dwords in q[0..3]) into the crop buffer at byte boff, the byte of
+// its first sample (boff = 0 mod 4 for an even lead, 2 mod 4 for an odd one: the sample pairs of
+// the crop buffer then straddle the word's dwords, realigned by v_alignbyte)
+__device__ __forceinline__ void crop_store_word(unsigned char *crop, const short8 *q, int boff, bool odd)
+{
+    uint32_t d[16];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const auto v = __builtin_bit_cast(uint4, q[k]);
+        d[4 * k] = v.x;
+        d[4 * k + 1] = v.y;
+        d[4 * k + 2] = v.z;
+        d[4 * k + 3] = v.w;
+    }
+    if (!odd) {
+        uint32_t *o = reinterpret_cast<uint32_t *>(crop + boff);
+#pragma unroll
+        for (int j = 0; j < 16; j++) o[j] = d[j];
+    } else {
+        *reinterpret_cast<uint16_t *>(crop + boff) = (uint16_t)d[0];
+        uint32_t *o = reinterpret_cast<uint32_t *>(crop + boff + 2);
+#pragma unroll
+        for (int j = 0; j < 15; j++) o[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], 2);
+        *reinterpret_cast<uint16_t *>(crop + boff + 62) = (uint16_t)(d[15] >> 16);
+    }
+}
+
+// One clip, FAST layout, not the exact redo; its RREG words are already in flight into regs (word
+// r * NT + tid in regs[4r .. 4r+3]).  Endpoint energies from exact moments, decisions certified;
+// returns false on a near tie (the clip is redone by extract_exact_kernel; no next-clip loads were
+// issued), true when done (the next clip's loads -- sh->next, resolved before the crop -- are in
+// flight in regs).
+template <typename Resolve>
+__device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, int i, const ClipRef &cur,
+                                          short8 (&regs)[NRV], Resolve resolve)
+{
+    Shared *sh = c.sh;
+#ifndef EXTRACT_FAST_OPAQUE
+#define EXTRACT_FAST_OPAQUE 1
+#endif
+    const int tid = EXTRACT_FAST_OPAQUE ? opaque_tid() : (int)threadIdx.x, lane = tid & 63,
+              wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int L = p.L, S = p.S;
+    asm volatile("" : "+s"(L), "+s"(S));  // per clip: constants derived from them are recomputed
+    const int n = cur.n, lead = cur.lead, nword = cur.nword;
+    const int oslot = i & (EXTRACT_OSTAGE - 1);
+    float *featb = c.ofeat + 15 * oslot;
+    STAMP(i, 0);
+#ifdef DSP_STAMPS
+    if (p.stamps) {  // diagnostic build: the clip's loads landed (stamp 13; per wave: 24 + wave)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        STAMP(i, 13);
+        if (lane == 0) p.stamps[(size_t)i * 32 + 24 + wid] = __builtin_amdgcn_s_memtime();
+    }
+#endif
+#if EXTRACT_SLOTS
+    const float invS = 1.0f / (float)S;
+    const int nv0 = (p.do_vad && n >= L) ? (n - L) / S + 1 : 0;  // = ClipStats::nv
+#endif
+
+    // ---- R1: integer sum / min / max; exact moments per word; the partial words of the frame ends
+    R1Acc acc = r1_acc_init();
+#pragma unroll
+    for (int r = 0; r < RREG; r++) {
+        const int w = r * NT + tid;
+        if (w < nword) {
+            r1_word(&regs[4 * r], w, nword, lead, n, acc, c.wS1, c.wS2);
+#if EXTRACT_SLOTS
+            if (nv0 > 0) {
+                int ts, te;
+                word_frame_ends(w, lead, L, S, invS, nv0, ts, te);
+                if (ts >= 0) store_slot(c.slots, ts, &regs[4 * r]);
+                if (te >= 0) store_slot(c.slots, te, &regs[4 * r]);
+            }
+#endif
+        }
+    }
+    r1_reduce(acc, sh, wid, lane);
+    __syncthreads();
+    if (tid == 0 && sh->sclear) {  // the last flush's slots (every thread has read them by now)
+        sh->smask = 0;
+        sh->schunk = -1;
+        sh->sclear = 0;
+    }
+    if (wid == 0) {  // the clip statistics once, shared through LDS
+        const ClipStats c0 = clip_stats(sh, n, L, S, p.do_vad);
+        if (lane == 0) sh->cs = {c0.mq, c0.Mp, c0.invM2, c0.invMf, c0.tpos, c0.t0, c0.nv};
+    }
+    __syncthreads();
+    ClipStats cs;
+    cs.mq = uni(sh->cs.mq);
+    cs.Mp = uni(sh->cs.Mp);
+    cs.invM2 = uni(sh->cs.invM2);
+    cs.invMf = uni(sh->cs.invMf);
+    cs.tpos = uni(sh->cs.tpos);
+    cs.t0 = uni(sh->cs.t0);
+    cs.nv = uni(sh->cs.nv);
+    const int nv = cs.nv;
+    STAMP(i, 1);
+
+    // ---- R2: positive-sample bits, one 32-bit word per 32 buffer samples ---------------------
+#pragma unroll
+    for (int r = 0; r < RREG; r++) {
+        const int w = r * NT + tid;
+        if (w < nword) c.posw[w] = (DSP_ABL & 4) ? 0u : pos_word(&regs[4 * r], w, nword, lead, n, cs.tpos);
+    }
+    if (tid < 2) c.posw[nword + tid] = 0;
+#if !EXTRACT_SLOTS
+    // the partial word of the frame end this thread sums in pass A (one frame end per thread),
+    // re-read from L2 and issued before the barrier so that it is in flight while the workgroup
+    // synchronises
+    short8 qa[4];
+    int pa_e0 = 0, pa_e1 = 0;
+    const int pa_w = vad_partial_issue(p, cur, L, S, nv, tid, qa, pa_e0, pa_e1);
+#endif
+    __syncthreads();
+    STAMP(i, 2);
+
+    // ---- R3: endpoint detection (:161-273) ------------------------------------------------
+    if (nv > 0) {
+#if EXTRACT_SLOTS
+        vad_frames_slots(c, cur, L, S, cs, tid);
+#else
+        vad_frames_fast(c, cur, L, S, cs, qa, pa_w, pa_e0, pa_e1, tid);
+#endif
+        STAMP(i, 7);
+        __syncthreads();
+        STAMP(i, 8);
+        if (wid == 0) {
+            // the workgroup's critical path (p90, then the scan) runs on this one wave: it takes
+            // issue priority over the co-resident workgroup's waves until the decisions are made
+            __builtin_amdgcn_s_setprio(2);
+            p90_select_wave(c, nv, lane);
+        }
+        if (wid == 1) vad_noise(c, nv, lane);  // beside wave 0's p90 selection
+        __syncthreads();
+        STAMP(i, 3);
+        if (wid == 0) {
+            const int flag = vad_scan<true, true>(p, c, nv, lane);
+            if (lane == 0) sh->exact = cs.Mp > 0.0 ? flag : 0;
+        }
+    }
+    if (tid == 0) {  // claimed at the clip's start (-1: none); its load range for the prefetch below
+        const int nx = resolve();
+        const ClipRef nr = nx >= 0 ? clip_ref(p, nx) : clip_none();
+        sh->next = nx;
+        sh->nx_base = nr.base;
+        sh->nx_nvec = nr.nvec;
+    }
+    if (wid == 0) __builtin_amdgcn_s_setprio(0);
+    __syncthreads();
+    int st = 0, en = n;
+    if (nv > 0) {
+        if (sh->exact) return false;  // near tie: redone in numpy's exact order by the exact kernel
+        if (sh->n3 >= 0) {
+            st = sh->n1 * S;              // :272
+            en = min(sh->n6 * S + L, n);  // :273
+        }
+        if (p.vad_energy)
+            for (int f = opaque_tid(); f < nv && f < p.ld_vad; f += NT) {
+                p.vad_energy[(size_t)i * p.ld_vad + f] = c.vE[f];
+                p.vad_zcr[(size_t)i * p.ld_vad + f] = c.vZ[f];
+            }
+    }
+    STAMP(i, 4);
+
+    // ---- the crop into LDS; the next clip's loads; R4 ---------------------------------------
+#if EXTRACT_CROP_DMA
+    // the crop's clip-relative vectors [st >> 3, (en - 1) >> 3] by LDS-DMA (buffer_load ... lds):
+    // 16-B loads at the clip's own alignment, each wave-instruction writing 1 KiB of LDS in lane
+    // order (no VGPRs, no LDS bank conflicts); crop vector v at LDS vector v - cv0.  They re-read
+    // the clip from L2; the clip's registers are dead here.
+    const int cv0 = st >> 3, cv1 = (en - 1) >> 3, sbase = 8 * cv0;
+    const bool in_lds = 16 * (cv1 - cv0 + 1) <= EXTRACT_CROP_BYTES;
+    // the last sample of a clip with an odd lead that ends on a vector boundary sits in a dword that
+    // straddles the descriptor's end, which a 16-B load drops: patched from the aligned vector
+    const int vfix = ((lead & 1) && ((lead + n) & 7) == 0) ? (n - 1) >> 3 : -1;
+    short klast = 0;
+#else
+    // the buffer words covering the crop's vectors [st >> 3, (en - 1) >> 3], copied whole from the
+    // registers: clip sample s at byte 2 (s - sbase), c0 = the first copied clip sample (>= -7),
+    // sbase = floor8(c0)
+    const int wf = ((st & ~7) + lead) >> 5, wl = (((en + 7) & ~7) - 1 + lead) >> 5;
+    const int c0 = 32 * wf - lead, sbase = (c0 >> 3) << 3;
+    const bool in_lds = 2 * (32 * (wl - wf + 1) + (c0 - sbase)) <= EXTRACT_CROP_BYTES;
+    const int vfix = -1;
+    const short klast = 0;
+#endif
+    int F = 0;
+    if (in_lds) {
+#if EXTRACT_CROP_DMA
+        const __amdgpu_buffer_rsrc_t rs = clip_rsrc(p, cur);
+        const int ncv = cv1 - cv0 + 1;
+        for (int j = 0; j * NT < ncv; j++) {  // wave-uniform trip count
+            const int v = cv0 + j * NT + tid;
+            if (v <= cv1)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void *)(c.crop + 16 * (j * NT + 64 * wid)), 16,
+                    2 * lead + 16 * v, 0, 0, 0);
+        }
+        if (vfix >= 0) klast = load_vec(p, cur, cur.nvec - 1)[7];
+#else
+#pragma unroll
+        for (int r = 0; r < RREG; r++) {
+            const int w = r * NT + tid;
+            if (w >= wf && w <= wl) crop_store_word(c.crop, &regs[4 * r], 64 * w - 2 * lead - 2 * sbase, lead & 1);
+        }
+#endif
+        // keep the next clip's loads below the copy (a compiler memory barrier: LDS stores and
+        // buffer loads do not alias, so the loads could be hoisted above the copy)
+        asm volatile("" ::: "memory");
+        STAMP(i, 14);
+    } else {
+        F = r4_frames<false, EXTRACT_R4F_KV>(p, c, cur, L, S, st, en, cs, sh->j0, sh->j1, 0, wid, lane);
+        STAMP(i, 12);
+        __syncthreads();
+    }
+    if (EXTRACT_FAST_PREFETCH) {
+        // the clip's registers are dead in both paths: the next clip's loads, issued at ONE place
+        // (one register assignment for the loop-carried words, no copies at the back edge); the
+        // range comes from LDS (a load of offsets[] here would wait for the crop DMAs)
+        ClipRef nr = clip_none();
+        nr.base = uni_ll(sh->nx_base);
+        nr.nvec = uni(sh->nx_nvec);
+        issue_clip(regs, p, nr, opaque_tid());
+    }
+    if (in_lds) {
+#if EXTRACT_CROP_DMA
+        // this wave's crop DMAs (and the patch load) have landed -- the NRV next-clip loads issued
+        // after them stay in flight -- then every wave's: a raw barrier (__syncthreads() would wait
+        // for the next clip's loads too)
+        static_assert(NRV == 12, "the counted wait below leaves NRV loads in flight");
+        asm volatile("s_waitcnt vmcnt(12)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+#else
+        __syncthreads();
+#endif
+        STAMP(i, 15);
+        F = r4_frames<true>(p, c, cur, L, S, st, en, cs, sh->j0, sh->j1, sbase >> 3, wid, lane, vfix, klast);
+        STAMP(i, 12);
+        __syncthreads();
+    }
+    STAMP(i, 5);
+
+    // ---- R5: 15-d statistics (compute_statistics x 3, fe.py:46-62) ------------------------
+    r5_fast(c, F, featb, wid, lane);
+    STAMP(i, 9);
+    if (p.seq)
+        for (int g = tid; g < F && g < p.ld_seq; g += NT) {
+            float *o = p.seq + ((size_t)i * p.ld_seq + g) * 3;
+            o[0] = c.fE[g];
+            o[1] = c.fM[g];
+            o[2] = (float)c.fZ[g];
+        }
+    if (tid == 0) {
+        c.ose[2 * oslot] = st;
+        c.ose[2 * oslot + 1] = en;
+        c.onf[oslot] = F;
+        c.ost[oslot] = DSP_CLIP_OK;
+        const int ch = i / EXTRACT_OSTAGE;  // the staged slots belong to chunk sh->schunk
+        const unsigned m0 = sh->schunk == ch ? sh->smask : 0u;
+        sh->schunk = ch;
+        sh->smask = m0 | (1u << oslot);
+    }
+    STAMP(i, 6);
+    return true;
+}
+
 __device__ __forceinline__ void write_bad_clip(const ExtractParams &p, int i, int tid)
 {
     if (tid < 15) p.feat[(size_t)i * 15 + tid] = __builtin_nanf("");
@@ -1357,6 +1774,8 @@ __device__ __forceinline__ Ctx ctx_from(const ExtractCarve &cv, unsigned char *l
     c.rank = reinterpret_cast<int *>(lds + cv.rank);
     c.pS1 = reinterpret_cast<int *>(lds + cv.pS1);
     c.pS2 = reinterpret_cast<unsigned long long *>(lds + cv.pS2);
+    c.slots = reinterpret_cast<short8 *>(lds + cv.slots);
+    c.crop = lds + cv.crop;
     c.ofeat = reinterpret_cast<float *>(lds + cv.ost);
     c.ose = reinterpret_cast<int32_t *>(lds + cv.ost + 4 * 15 * EXTRACT_OSTAGE);
     c.onf = c.ose + 2 * EXTRACT_OSTAGE;
@@ -1440,10 +1859,10 @@ __device__ __forceinline__ void flush_outputs(const ExtractParams &p, const Ctx 
     }
 }
 
-// FAST launches run extract_kernel<true>, one clip at a time per workgroup.  A two-clip pipeline
-// (the single-wave phases of one clip beside the multi-wave phases of the other, round 4) measured
-// 3.41 against 3.35 ms: the CU is bound by instruction issue and the pipeline added 10% VALU and
-// 49% SALU instructions (profiles/r04d_*), so it was removed.
+// FAST launches run extract_kernel<true>, one clip at a time per workgroup (clip_fast).  A two-clip
+// pipeline (the single-wave phases of one clip beside the multi-wave phases of the other, round 4)
+// measured 3.41 against 3.35 ms: it added 10% VALU and 49% SALU instructions, and was removed
+// (the A/B's raw record was not kept).
 
 // 128 VGPRs: two 512-thread workgroups per CU
 #ifndef EXTRACT_WAVES_PER_EU
@@ -1462,40 +1881,51 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     WG_STAMP(16);
     build_window(p, c, tid, lane, wid);
+    WG_CK(18);
     const ClipQueue Q = queue_open(p, sh);
     if (tid == 0) {
         sh->next = queue_next(Q, sh);
         sh->smask = 0;
         sh->schunk = -1;
+        sh->sclear = 0;
     }
     __syncthreads();
+    WG_CK(19);
     short8 regs[NRV];
-    bool inflight = false;  // regs already hold clip i's loads (issued by the previous clip's R4)
+    bool inflight = false;  // regs already hold clip i's loads (issued by the previous clip)
     for (int i = sh->next; i >= 0;) {
         const ClipRef cur = clip_ref(p, i);
         if (!cur.ok) {
-            __syncthreads();  // everyone has read sh->next (the ok path has barriers in clip_body)
+            __syncthreads();  // everyone has read sh->next (the ok path has barriers in its body)
             if (tid == 0) sh->next = queue_next(Q, sh);
-            write_bad_clip(p, i, tid);
+            write_bad_clip(p, i, opaque_tid());
             inflight = false;
         } else {
-            if (!inflight) issue_clip(regs, p, cur);
+            if (!inflight) issue_clip(regs, p, cur, opaque_tid());
             unsigned cl = 0;
             if (tid == 0) cl = queue_begin(Q, sh);
             c.stamp_clip = i;
-            const bool done = clip_body<false, FAST>(p, c, i, cur, regs, [&]() { return queue_end(Q, sh, cl); });
-            if (!done) {  // a deferred clip returns before R4
-                if (tid == 0) {
-                    p.status[i] = DSP_CLIP_UNCERTIFIED;
-                    sh->next = queue_end(Q, sh, cl);
-                }
+            bool done;
+            if constexpr (FAST) {
+                // resolves sh->next itself (before the crop), also for a deferred clip
+                done = clip_fast(p, c, i, cur, regs, [&]() { return queue_end(Q, sh, cl); });
+            } else {
+                done = clip_body<false, false>(p, c, i, cur, regs, [&]() { return queue_end(Q, sh, cl); });
+                if (!done && tid == 0) sh->next = queue_end(Q, sh, cl);  // a deferred clip returns before R4
             }
-            inflight = EXTRACT_PREFETCH && done;
+            if (!done && tid == 0) {
+                p.status[i] = DSP_CLIP_UNCERTIFIED;
+                if (p.queue) __hip_atomic_fetch_add(p.queue + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            inflight = (FAST ? EXTRACT_FAST_PREFETCH : EXTRACT_PREFETCH) && done;
         }
         __syncthreads();  // LDS summaries are rewritten by the next clip; sh->next published
         const int prev = i;
         i = sh->next;
-        if (i < 0 || (i ^ prev) >= EXTRACT_OSTAGE) flush_outputs(p, c, prev, tid);  // next clip in another chunk
+        if (i < 0 || (i ^ prev) >= EXTRACT_OSTAGE) {  // next clip in another chunk
+            flush_outputs(p, c, prev, opaque_tid());  // (addresses computed here, not hoisted and spilled)
+            if (tid == 0) sh->sclear = 1;
+        }
     }
     if (tid == 0) queue_done(p);
     WG_STAMP(22);
@@ -1503,10 +1933,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVE
 
 // Launched after extract_kernel on the same stream: every clip they left
 // DSP_CLIP_UNCERTIFIED (rare) is redone from the start by one workgroup, on the bit-exact
-// (numpy-order) energy path, and gets its final outputs and DSP_CLIP_FLAG_VAD_EXACT.
+// (numpy-order) energy path, and gets its final outputs and DSP_CLIP_FLAG_VAD_EXACT.  With the
+// clip queue, extract_kernel counts its near ties in queue word 9: a launch with none returns at
+// once (one load per workgroup); otherwise the last workgroup out zeroes words 9 and 10 again.
 template <bool FAST>
 __global__ __launch_bounds__(NT) void extract_exact_kernel(ExtractParams p)
 {
+    if (p.queue && __hip_atomic_load(p.queue + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     Ctx c = make_ctx<FAST>(p, lds);
     Shared *sh = c.sh;
@@ -1535,6 +1968,13 @@ __global__ __launch_bounds__(NT) void extract_exact_kernel(ExtractParams p)
             issue_clip(regs, p, cr);
             clip_body<true, FAST>(p, c, ci, cr, regs);
             __syncthreads();
+        }
+    }
+    if (p.queue && tid == 0) {  // every workgroup has read word 9 before its increment of word 10
+        const unsigned d = __hip_atomic_fetch_add(p.queue + 10, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (d == gridDim.x - 1) {
+            __hip_atomic_store(p.queue + 9, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(p.queue + 10, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }

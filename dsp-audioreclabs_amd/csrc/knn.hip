@@ -213,9 +213,11 @@ typedef float mq_f4 __attribute__((ext_vector_type(4)));
 // below min(seed, the lists' thresholds); knn_merge starts its screening cut-off at the seed, so a
 // query whose seed was too tight fails certification and is answered by the exhaustive fallback:
 // exactness never depends on the seed.
-// The same kernel screens that sample (the pilot): rows are the sample's, sample row j = reference
-// row j * rstride (rstride = 1: every row), and the query's own row is masked in global numbering.
-template <int DP, int KC>
+// The same kernel screens that sample (the pilot; PILOT only names the instantiation, so that a
+// profile separates the pilot from the main screen): rows are the sample's, sample row j =
+// reference row j * rstride (rstride = 1: every row), and the query's own row is masked in global
+// numbering.
+template <int DP, int KC, bool PILOT = false>
 __global__ __launch_bounds__(64 * MQ_W) void knn_screen_mfma(const float *__restrict__ ref32, int64_t Nr,
                                                            const float *__restrict__ q32, int64_t Nq,
                                                            int64_t self_offset, int nsplit,
@@ -347,10 +349,13 @@ __global__ __launch_bounds__(64 * MQ_W) void knn_screen_mfma(const float *__rest
 }
 
 // the seed of each query: the KC-th smallest of the pilot's nsplit x KC screened distances (the KC
-// smallest of the sample), one thread per query
+// smallest of the sample), one thread per query.  A pilot that was itself seeded (prev) kept only
+// distances below prev[q]: its KC-th is then either the sample's own KC-th (< prev) or +inf (the
+// sample's KC-th is >= prev), so the seed is the smaller of the two -- an upper bound either way.
 template <int KC>
 __global__ __launch_bounds__(256) void knn_seed(const float *__restrict__ cand_d, int nsplit, int64_t Nq,
-                                                float *__restrict__ seed, float scale)
+                                                const float *__restrict__ prev, float *__restrict__ seed,
+                                                float scale)
 {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= Nq) return;
@@ -370,7 +375,8 @@ __global__ __launch_bounds__(256) void knn_seed(const float *__restrict__ cand_d
             }
         }
     }
-    seed[q] = k32[KC - 1] * scale;  // scale: 1 (< 1 only in the diagnostic build's tests)
+    const float kth = prev ? fminf(k32[KC - 1], prev[q]) : k32[KC - 1];
+    seed[q] = kth * scale;  // scale: 1 (< 1 only in the diagnostic build's tests, final stage)
 }
 
 // High-dimensional rows (D > 32: the sequence method's flattened (E, ZCR) sequences,
@@ -935,19 +941,25 @@ __global__ void zscore_apply_kernel(const double *X, int64_t N, int D, const dou
 // ------------------------------------------------------------------------------------------
 namespace {
 struct KnnLayout {
-    size_t ref32, q32, cand_d, cand_i, misc, pilot_d, seed, total;
+    size_t ref32, q32, cand_d, cand_i, misc, pilot_d, seed0, seed, total;
     int DP, KC, nsplit;
     int rstride, nsample, nsplit_p;  // seeded thresholds (rstride > 0): sample rows j * rstride
+    int rstride0, nsample0;          // the pilot's own seed: a smaller sample (rows j * rstride0)
     bool exp;  // expanded-form screening (a spare padded column holds |r|^2)
     bool hd;   // D > 32: chunked direct-form screen (knn_screen_hd)
     bool mfma; // expanded form on the matrix cores (knn_screen_mfma)
 };
 
 static constexpr int KNN_DMAX = 4096;
-// seeded thresholds: a pilot over ~KNN_SEED_SAMPLE strided rows when the set has >= KNN_SEED_MIN_NR;
-// the split model's warm-up term after seeding (rows)
+// seeded thresholds: a pilot over ~KNN_SEED_SAMPLE strided rows when the set has >= KNN_SEED_MIN_NR,
+// itself seeded by a pre-pilot over ~KNN_SEED_SAMPLE0 rows (a pilot from +inf thresholds is all
+// list warm-up: 84 us of a 0.8 ms job at 12.5k x 100k for 4% of the pairs); the split model's
+// warm-up term after seeding (rows)
 #ifndef KNN_SEED_SAMPLE
-#define KNN_SEED_SAMPLE 4096
+#define KNN_SEED_SAMPLE 2048
+#endif
+#ifndef KNN_SEED_SAMPLE0
+#define KNN_SEED_SAMPLE0 256
 #endif
 #ifndef KNN_SEED_MIN_NR
 #define KNN_SEED_MIN_NR 32768
@@ -1041,12 +1053,14 @@ KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
 
     // seeded thresholds (matrix-core screen, reference sets of >= KNN_SEED_MIN_NR rows): a pilot
     // screen over every rstride-th row (~KNN_SEED_SAMPLE rows) seeds each query's threshold
-    l.rstride = 0;
-    l.nsample = 0;
+    l.rstride = l.rstride0 = 0;
+    l.nsample = l.nsample0 = 0;
     l.nsplit_p = 0;
     if (l.mfma && Nr >= KNN_SEED_MIN_NR) {
         l.rstride = (int)std::max<int64_t>(2, Nr / KNN_SEED_SAMPLE);
         l.nsample = (int)((Nr + l.rstride - 1) / l.rstride);
+        l.rstride0 = (int)std::max<int64_t>(2, Nr / KNN_SEED_SAMPLE0);
+        l.nsample0 = (int)((Nr + l.rstride0 - 1) / l.rstride0);
     }
 #ifdef DSP_KNN_DIAG  // diagnostic build only: seeding off (DSP_KNN_SEED=0)
     if (const char *e = getenv("DSP_KNN_SEED"))
@@ -1072,13 +1086,14 @@ KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
     l.cand_d = o; o += al((size_t)l.nsplit * Nq * l.KC * 4);
     l.cand_i = o; o += al((size_t)l.nsplit * Nq * l.KC * 4);
     l.misc = o;  o += al(16 + (size_t)Nq * 4);   // maxnorm bits, fallback count, fallback list
-    l.pilot_d = l.seed = 0;
+    l.pilot_d = l.seed0 = l.seed = 0;
     if (l.rstride) {
         // pilot splits: enough workgroups to fill the chip twice over, >= one tile of rows each
         const int64_t qblocks = (Nq + dsp::mq_qpb(l.KC) - 1) / dsp::mq_qpb(l.KC);
         l.nsplit_p = (int)std::max<int64_t>(1, std::min<int64_t>({(2 * device_cus() + qblocks - 1) / qblocks,
                                                                   (l.nsample + dsp::MQ_TR - 1) / dsp::MQ_TR, 64}));
-        l.pilot_d = o; o += al((size_t)l.nsplit_p * Nq * l.KC * 4);
+        l.pilot_d = o; o += al((size_t)l.nsplit_p * Nq * l.KC * 4);  // (the pre-pilot: one split)
+        l.seed0 = o;   o += al((size_t)Nq * 4);
         l.seed = o;    o += al((size_t)Nq * 4);
     }
     l.total = o;
@@ -1205,9 +1220,9 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
         const int qpb = dsp::mq_qpb(l.KC);
         const unsigned qb = (unsigned)((Nq + qpb - 1) / qpb);
         const dim3 b(64 * dsp::MQ_W);
-#define DSP_SCREEN_MQ(DPV, KCV, G, NR, NS, CD, CI, RSTR, SEED)                                     \
+#define DSP_SCREEN_MQ(DPV, KCV, PIL, G, NR, NS, CD, CI, RSTR, SEED)                                \
     if (l.DP == DPV && l.KC == KCV)                                                               \
-    hipLaunchKernelGGL((dsp::knn_screen_mfma<DPV, KCV>), G, b, 0, s, ref32, NR, q32, Nq, self_offset, NS, \
+    hipLaunchKernelGGL((dsp::knn_screen_mfma<DPV, KCV, PIL>), G, b, 0, s, ref32, NR, q32, Nq, self_offset, NS, \
                        CD, CI, RSTR, SEED)
 #define DSP_SCREEN_MQ_ALL(...)                                                                    \
         DSP_SCREEN_MQ(16, 8, __VA_ARGS__); DSP_SCREEN_MQ(16, 16, __VA_ARGS__); DSP_SCREEN_MQ(16, 24, __VA_ARGS__); \
@@ -1219,21 +1234,29 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
 #ifdef DSP_KNN_DIAG  // diagnostic build only: an adversarially tight seed (fallback tests)
             if (const char *e = getenv("DSP_KNN_SEED_SCALE")) seed_scale = (float)atof(e);
 #endif
-            // pilot over the sampled rows (same kernel, same fp32 arithmetic), then the seeds
+            // pilots over the sampled rows (same kernel, same fp32 arithmetic): a pre-pilot over
+            // nsample0 rows from +inf thresholds seeds the pilot over nsample rows, whose seeds
+            // start the main screen
             float *pd = (float *)(ws + l.pilot_d);
-            const dim3 gp(qb, (unsigned)l.nsplit_p);
-            DSP_SCREEN_MQ_ALL(gp, (int64_t)l.nsample, l.nsplit_p, pd, (int *)nullptr, l.rstride, (const float *)nullptr);
+            float *seed0 = (float *)(ws + l.seed0);
             const dim3 gs((unsigned)((Nq + 255) / 256));
-            switch (l.KC) {
-            case 6: hipLaunchKernelGGL((dsp::knn_seed<6>), gs, dim3(256), 0, s, pd, l.nsplit_p, Nq, seedp, seed_scale); break;
-            case 8: hipLaunchKernelGGL((dsp::knn_seed<8>), gs, dim3(256), 0, s, pd, l.nsplit_p, Nq, seedp, seed_scale); break;
-            case 16: hipLaunchKernelGGL((dsp::knn_seed<16>), gs, dim3(256), 0, s, pd, l.nsplit_p, Nq, seedp, seed_scale); break;
-            case 24: hipLaunchKernelGGL((dsp::knn_seed<24>), gs, dim3(256), 0, s, pd, l.nsplit_p, Nq, seedp, seed_scale); break;
-            default: hipLaunchKernelGGL((dsp::knn_seed<36>), gs, dim3(256), 0, s, pd, l.nsplit_p, Nq, seedp, seed_scale); break;
-            }
+            auto seeds = [&](int nsp, const float *prev, float *out, float scale) {
+                switch (l.KC) {
+                case 6: hipLaunchKernelGGL((dsp::knn_seed<6>), gs, dim3(256), 0, s, pd, nsp, Nq, prev, out, scale); break;
+                case 8: hipLaunchKernelGGL((dsp::knn_seed<8>), gs, dim3(256), 0, s, pd, nsp, Nq, prev, out, scale); break;
+                case 16: hipLaunchKernelGGL((dsp::knn_seed<16>), gs, dim3(256), 0, s, pd, nsp, Nq, prev, out, scale); break;
+                case 24: hipLaunchKernelGGL((dsp::knn_seed<24>), gs, dim3(256), 0, s, pd, nsp, Nq, prev, out, scale); break;
+                default: hipLaunchKernelGGL((dsp::knn_seed<36>), gs, dim3(256), 0, s, pd, nsp, Nq, prev, out, scale); break;
+                }
+            };
+            const dim3 gp0(qb, 1u), gp(qb, (unsigned)l.nsplit_p);
+            DSP_SCREEN_MQ_ALL(true, gp0, (int64_t)l.nsample0, 1, pd, (int *)nullptr, l.rstride0, (const float *)nullptr);
+            seeds(1, nullptr, seed0, 1.f);
+            DSP_SCREEN_MQ_ALL(true, gp, (int64_t)l.nsample, l.nsplit_p, pd, (int *)nullptr, l.rstride, (const float *)seed0);
+            seeds(l.nsplit_p, seed0, seedp, seed_scale);
         }
         const dim3 g(qb, (unsigned)l.nsplit);
-        DSP_SCREEN_MQ_ALL(g, Nr, l.nsplit, cd, ci, 1, (const float *)seedp);
+        DSP_SCREEN_MQ_ALL(false, g, Nr, l.nsplit, cd, ci, 1, (const float *)seedp);
 #undef DSP_SCREEN_MQ_ALL
 #undef DSP_SCREEN_MQ
     } else {

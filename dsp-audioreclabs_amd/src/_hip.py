@@ -55,6 +55,16 @@ def load_library(path=LIB_PATH):
                        "`python -c 'import __graft_entry__ as g; g.build()'` in the repo root" % path)
     L = ctypes.CDLL(path)
     vp, i64, i32, dbl, sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double, ctypes.c_size_t
+    # the ABI version first: a stale library then fails with "rebuild it", not with a missing symbol
+    L.dsp_abi_version.restype = i32
+    L.dsp_abi_version.argtypes = []
+    # DSP_ABI_ANY=1: A/B tools loading an older variant library (tools/ab_bench.sh); the queue
+    # scratch this binding passes (64 zero bytes) serves ABI 2's 8-byte counter pair too
+    if L.dsp_abi_version() != ABI_VERSION and not (os.environ.get("DSP_ABI_ANY") == "1" and L.dsp_abi_version() >= 2):
+        raise HipError("%s has ABI %d, this binding expects %d: rebuild it" % (path, L.dsp_abi_version(), ABI_VERSION))
+    missing = [e for e in EXPORTS if not hasattr(L, e)]
+    if missing and os.environ.get("DSP_ABI_ANY") != "1":
+        raise HipError("%s lacks %s: rebuild it" % (path, ", ".join(missing)))
     L.dsp_extract_lds_bytes.restype = sz
     L.dsp_extract_lds_bytes.argtypes = [i64, i32, i32]
     L.dsp_extract_features.restype = i32
@@ -76,12 +86,6 @@ def load_library(path=LIB_PATH):
     L.dsp_zscore_fit.argtypes = [vp, i64, i32, vp, vp, vp]
     L.dsp_zscore_apply.restype = i32
     L.dsp_zscore_apply.argtypes = [vp, i64, i32, vp, vp, vp, vp]
-    L.dsp_abi_version.restype = i32
-    L.dsp_abi_version.argtypes = []
-    # DSP_ABI_ANY=1: A/B tools loading an older variant library (tools/ab_bench.sh); the queue
-    # scratch this binding passes (64 zero bytes) serves ABI 2's 8-byte counter pair too
-    if L.dsp_abi_version() != ABI_VERSION and not (os.environ.get("DSP_ABI_ANY") == "1" and L.dsp_abi_version() >= 2):
-        raise HipError("%s has ABI %d, this binding expects %d: rebuild it" % (path, L.dsp_abi_version(), ABI_VERSION))
     _lib = L
     return L
 

@@ -44,13 +44,55 @@ def decode_pcm_bytes(raw, sample_width, n_channels):
     return audio, ints, scale
 
 
-def _read_wav(filepath):
+def _read_wav_module(filepath):
+    """The reference's reader (src/audio_processing.py:20-28): Python's wave module."""
     with wave.open(filepath, "rb") as w:
         n_channels = w.getnchannels()
         sample_width = w.getsampwidth()
         sample_rate = w.getframerate()
         raw = w.readframes(w.getnframes())
     return raw, sample_width, n_channels, sample_rate
+
+
+def _parse_riff(buf):
+    """The data bytes and format of a well-formed PCM WAV image, exactly what wave.open +
+    readframes(getnframes()) return for it (RIFF/WAVE header, chunks padded to even sizes, 'fmt '
+    with WAVE_FORMAT_PCM before 'data', nframes = data size // frame size); None for anything
+    else -- the caller then takes the wave module itself, errors and all."""
+    if len(buf) < 12 or buf[0:4] != b"RIFF" or buf[8:12] != b"WAVE":
+        return None
+    p, n, fmt = 12, len(buf), None
+    while p + 8 <= n:
+        cid, size = buf[p:p + 4], int.from_bytes(buf[p + 4:p + 8], "little")
+        body = p + 8
+        if cid == b"fmt ":
+            if size < 16 or body + 16 > n:
+                return None
+            tag, ch, sr = int.from_bytes(buf[body:body + 2], "little"), int.from_bytes(buf[body + 2:body + 4], "little"), \
+                int.from_bytes(buf[body + 4:body + 8], "little")
+            bits = int.from_bytes(buf[body + 14:body + 16], "little")
+            if tag != 1 or ch == 0 or bits == 0:
+                return None
+            fmt = (ch, (bits + 7) // 8, sr)
+        elif cid == b"data":
+            if fmt is None:
+                return None
+            ch, sw, sr = fmt
+            nbytes = (size // (ch * sw)) * ch * sw
+            if body + nbytes > n:  # truncated file: the wave module's own behaviour
+                return None
+            return memoryview(buf)[body:body + nbytes], sw, ch, sr
+        p = body + size + (size & 1)
+    return None
+
+
+def _read_wav(filepath):
+    """(data bytes, sample width, channels, sample rate) of a WAV file: one read and a RIFF chunk
+    walk for well-formed PCM files, the wave module (the reference's reader) for anything else."""
+    with open(filepath, "rb") as f:
+        buf = f.read()
+    r = _parse_riff(buf)
+    return r if r is not None else _read_wav_module(filepath)
 
 
 def load_wav(filepath):
@@ -67,6 +109,8 @@ def load_wav_pcm(filepath):
     which preprocess cancels): int16 for 16-bit mono and 8-bit mono/stereo; for 16-bit stereo the
     channel sums, int16 when they fit and int32 otherwise (17 bits: dsp_extract_general)."""
     raw, sw, ch, sr = _read_wav(filepath)
+    if sw == 2 and ch == 1:  # the common case: the payload itself, no conversion
+        return np.frombuffer(raw, dtype=np.int16), sr
     _, ints, _ = decode_pcm_bytes(raw, sw, ch)
     if ints.size and (ints.max() > 32767 or ints.min() < -32768):
         return ints.astype(np.int32), sr

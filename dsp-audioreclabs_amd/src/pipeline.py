@@ -54,6 +54,15 @@ class FeatureExtractor:
         self.return_sequences = return_sequences
         self._bufs = {}
 
+    def _queue_ws(self):
+        """The zeroed DSP_QUEUE_WS_BYTES scratch of this extractor's launches (stream-ordered
+        reuse: one extractor is not meant to launch on two streams at once)."""
+        import torch
+        q = getattr(self, "_queue", None)
+        if q is None:
+            q = self._queue = torch.zeros(_hip.QUEUE_WS_BYTES // 4, dtype=torch.int32, device=self.device)
+        return q
+
     def lds_bytes(self, max_len):
         return _hip.lib().dsp_extract_lds_bytes(int(max_len), self.L, self.S)
 
@@ -141,9 +150,10 @@ class FeatureExtractor:
                 _hip.ptr(sq), lds_)
         cap = 0 if wide else self.fused_cap()
         if not wide and B > 0 and cap > 0:
-            # the launch's own zeroed clip-queue counter pair: a capture of this call in a graph
-            # gets its own from the graph's pool, so concurrent launches never share one
-            queue = torch.zeros(_hip.QUEUE_WS_BYTES // 4, dtype=torch.int32, device=d)
+            # the clip-queue scratch: zeroed once, and every launch leaves it zeroed again (the
+            # last workgroup out of each kernel resets its counters), so the launches of this
+            # extractor on its stream reuse one buffer without a fill kernel per call
+            queue = self._queue_ws()
             rc = _hip.lib().dsp_extract_features(
                 _hip.ptr(pcm), _hip.ptr(off), B, min(max_len, cap), self.L, self.S,
                 _hip.ptr(self.window), *args, _hip.ptr(queue), _hip.stream_handle(d))

@@ -63,9 +63,12 @@ extern "C" {
 size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int frame_shift);
 
 /*
- * dsp_extract_features -- fused per-clip pipeline: persistent workgroups (two per CU), each
- * keeping two clips in flight (one in registers, one in LDS summaries), then a second launch on
- * the same stream that redoes near-tie endpoint decisions on the bit-exact path.
+ * dsp_extract_features -- fused per-clip pipeline: persistent workgroups (two per CU), each taking
+ * one clip at a time from a clip queue, the clip held in registers until its endpoints are
+ * decided; the crop is then copied into LDS and the registers take the next clip's loads while
+ * the crop frames and statistics are computed.  A second launch on the same stream redoes
+ * near-tie endpoint decisions on the bit-exact path (it returns at once when the first counted
+ * none in queue_ws).
  * Replaces, per clip, the chain
  *   preprocess            src/audio_processing.py:78-90   (remove_dc :49-59, normalize_audio :62-75)
  *   endpoint_detection    src/audio_processing.py:135-275 (when do_vad != 0)

@@ -171,10 +171,11 @@ def test_sharded_knn_self_query_equals_single():
 
 
 def test_many_near_ties():
-    """Near ties under pressure: every third clip of a 5G + 37-clip batch is a near tie, so both
-    slots of the fused kernel's two-clip pipeline hit them back to back.  Each is left
-    DSP_CLIP_UNCERTIFIED by extract_pipe_kernel and redone by extract_exact_kernel on the same
-    stream: every clip must match the oracle and every near tie carry DSP_CLIP_FLAG_VAD_EXACT."""
+    """Near ties under pressure: every third clip of a 5G + 37-clip batch is a near tie, so every
+    workgroup of the fused kernel meets several of them, between clips whose next-clip loads are in
+    flight.  Each is left DSP_CLIP_UNCERTIFIED by extract_kernel (and counted in queue_ws) and
+    redone by extract_exact_kernel on the same stream: every clip must match the oracle and every
+    near tie carry DSP_CLIP_FLAG_VAD_EXACT."""
     import torch
     from src.pipeline import FeatureExtractor, create_window
     from src.synth import make_batch

@@ -76,3 +76,48 @@ def test_shard_range_partitions():
             assert max(sizes) - min(sizes) <= 1
     with pytest.raises(ValueError):
         shard_range(10, 2, 2)
+
+
+def _riff(chunks):
+    body = b"WAVE" + b"".join(cid + len(d).to_bytes(4, "little") + d + (b"\0" if len(d) & 1 else b"")
+                              for cid, d in chunks)
+    return b"RIFF" + len(body).to_bytes(4, "little") + body
+
+
+def _fmt(tag, ch, sr, bits):
+    import struct
+    return struct.pack("<HHLLHH", tag, ch, sr, sr * ch * ((bits + 7) // 8), ch * ((bits + 7) // 8), bits)
+
+
+def test_riff_reader_equals_wave_module(tmp_path):
+    """The one-read RIFF walk (load_wav_pcm's reader) returns exactly what the reference's
+    wave.open + readframes(getnframes()) returns (src/audio_processing.py:20-28), and files it does
+    not take (non-PCM, data before fmt, truncated) go to the wave module with its errors."""
+    from src.audio_processing import _read_wav, _read_wav_module, load_wav_pcm
+    rng = np.random.default_rng(1)
+    pcm = rng.integers(-32768, 32768, 2001, dtype=np.int16).tobytes()
+    cases = {
+        "mono16": _riff([(b"fmt ", _fmt(1, 1, 44100, 16)), (b"data", pcm)]),
+        "stereo16_partial_frame": _riff([(b"fmt ", _fmt(1, 2, 22050, 16)), (b"data", pcm)]),  # 4002 B: 1000 frames + 2
+        "mono8_odd_list": _riff([(b"fmt ", _fmt(1, 1, 8000, 8)), (b"LIST", b"abc"), (b"data", pcm[:777])]),
+        "fmt18": _riff([(b"fmt ", _fmt(1, 1, 44100, 16) + b"\0\0"), (b"data", pcm[:100])]),
+        "float": _riff([(b"fmt ", _fmt(3, 1, 44100, 32)), (b"data", pcm[:400])]),
+        "data_first": _riff([(b"data", pcm[:100]), (b"fmt ", _fmt(1, 1, 44100, 16))]),
+        "truncated": _riff([(b"fmt ", _fmt(1, 1, 44100, 16)), (b"data", pcm)])[:-500],
+        "bits24": _riff([(b"fmt ", _fmt(1, 1, 44100, 24)), (b"data", pcm[:999])]),
+        "not_riff": b"RIFX" + b"\0" * 40,
+    }
+    for name, blob in cases.items():
+        p = tmp_path / (name + ".wav")
+        p.write_bytes(blob)
+        try:
+            want = _read_wav_module(str(p))
+        except Exception as e:  # noqa: BLE001
+            with pytest.raises(type(e)):
+                _read_wav(str(p))
+            continue
+        got = _read_wav(str(p))
+        assert bytes(got[0]) == bytes(want[0]) and tuple(got[1:]) == tuple(want[1:]), name
+    x = np.frombuffer(pcm, np.int16)
+    got, sr = load_wav_pcm(str(tmp_path / "mono16.wav"))
+    assert sr == 44100 and got.dtype == np.int16 and np.array_equal(got, x)

@@ -11,16 +11,20 @@ C = len(st)
 print("workgroups %d  clock %.3f GHz" % (G, ghz))
 dur = (rt1 - rt0) / 100
 print("wg us  p0 %.2f p50 %.2f p90 %.2f max %.2f" % tuple(np.percentile(dur, [0, 50, 90, 100])))
-print("prologue us  p50 %.2f max %.2f" % (np.median((st[:G, 0] - ck0) / cyc), ((st[:G, 0] - ck0) / cyc).max()))
-for k, nm in ((18, "window loads issued"), (19, "pads + barrier"), (20, "weights + barrier"), (0, "first clip issued")):
-    print("  prologue %-20s p50 %.2f" % (nm, np.median((st[:G, k] - ck0) / cyc)))
+# prologue, from the workgroup's own row (one clock): entry (17) -> window built (18) -> first
+# clip claimed (19); clip rows are not the workgroup's (the queue hands out the first clip)
+pro = (st[:G, 19] - ck0) / cyc
+print("prologue us  p50 %.2f max %.2f  (window built p50 %.2f)" % (
+    np.median(pro), pro.max(), np.median((st[:G, 18] - ck0) / cyc)))
 tot = (st[:, 6] - st[:, 0]) / cyc
 print("clip us  p50 %.2f p90 %.2f | first round p50 %.2f (wg<%d %.2f, wg>=%d %.2f) later %.2f" % (
     np.median(tot), np.percentile(tot, 90), np.median(tot[:G]), G // 2, np.median(tot[:G // 2]), G // 2,
     np.median(tot[G // 2:G]), np.median(tot[G:]) if C > G else 0))
 names = {13: "R1 load wait", 1: "R1 stats", 2: "R2 pos", 7: "VAD pass A", 8: "VAD pass B", 3: "p90", 10: "noise+thr", 11: "scan",
-         4: "vad out", 12: "R4 frames", 5: "R4 barrier+issue", 9: "R5 jobs", 6: "R5 out"}
-seq = [0, 13, 1, 2, 7, 8, 3, 10, 11, 4, 12, 5, 9, 6]
+         4: "vad out", 14: "crop copy", 15: "issue+barrier", 12: "R4 frames", 5: "R4 barrier(+issue)", 9: "R5 jobs",
+         6: "R5 out"}
+# the crop stamps (14, 15) exist only for clips whose crop went to LDS
+seq = [0, 13, 1, 2, 7, 8, 3, 10, 11, 4] + ([14, 15] if (st[:, 14] > 0).any() else []) + [12, 5, 9, 6]
 for a, b in zip(seq, seq[1:]):
     d = (st[:, b] - st[:, a]) / cyc
     print("  %-14s p50 %.2f  oldWG %.2f newWG %.2f" % (names[b], np.median(d), np.median(d[:G // 2]), np.median(d[G // 2:G])))
