@@ -135,8 +135,6 @@ struct Shared {
     int qnext, qend, qcursor, qrange;  // clip queue (thread 0): the current chunk's next clip and end;
                                        // static split cursor; ranges used up
     int cdir, cy;                      // the pending claim (queue_begin / queue_end)
-    long long nx_base;                 // clip_fast: the next clip's load range (clip_ref), read by
-    int nx_nvec;                       // thread 0 when it resolves the claim
     unsigned smask;                    // staged output slots (ost) ...
     int schunk;                        // ... of this chunk
     int sclear;                        // the staged slots were flushed: thread 0 clears smask after
@@ -185,8 +183,6 @@ struct Ctx {
     int *rank;  // rank scratch: nvcap or 3 * fcap ints
     int *pS1;   // partial-word moments at the two ends of each VAD frame (2 * nvcap)
     unsigned long long *pS2;
-    short8 *slots;   // FAST: the 32-sample word of each partial VAD frame end t (4 vectors at slots[4t])
-    unsigned char *crop;  // FAST: crop buffer (clip sample s at byte 2 (s - sbase), sbase = 0 mod 8)
     float *ofeat;    // staged outputs of the clips of one chunk, slot = clip mod EXTRACT_OSTAGE:
     int32_t *ose;    // feat [slot][15], start/end [slot][2], n_frames [slot], status [slot]
     int32_t *onf, *ost;
@@ -528,11 +524,6 @@ __device__ __forceinline__ float uni(float v)
 {
     return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
 }
-__device__ __forceinline__ long long uni_ll(long long v)
-{
-    const unsigned lo = __builtin_amdgcn_readfirstlane((int)v), hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
-    return (long long)(((unsigned long long)hi << 32) | lo);
-}
 __device__ __forceinline__ double uni(double v)
 {
     const long long b = __builtin_bit_cast(long long, v);
@@ -773,26 +764,17 @@ __device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur
 }
 
 // R4: windowed frames over the crop [st, en) (:378, :299-333; fe.py:12-43) -> c.fE / fM / fZ.
-// One 16-lane row per frame (4 frames per wave), in the canonical order of dsp_device.h: lane rl
-// takes the frame's clip-relative 8-sample vectors va + rl + 16k, so the sums do not depend on
-// where the clip sits in the buffer and equal dsp_extract_general's.  The vectors come from the
-// LDS crop buffer (FROM_LDS: 16-B aligned there, vector v at crop vector v - sb8) or are re-read from
-// L2 (16-B loads at the clip's own 2-byte alignment).  Per sample y = w_j x (the reference's windowed
-// frame, :329-331), E += y^2, M += |y|; the weights of a vector's 8 samples are two aligned 16-B
-// reads from the window copy shifted by fs mod 4.  Returns F.
+// One 16-lane row per frame (4 frames per wave), in the canonical order of dsp_device.h: the
+// frame's clip-relative 8-sample vectors are re-read from L2 (16-B loads at the clip's own 2-byte
+// alignment) and lane rl takes vectors va + rl + 16k, so the sums do not depend on where the clip
+// sits in the buffer and equal dsp_extract_general's.  Per sample y = w_j x (the reference's
+// windowed frame, :329-331), E += y^2, M += |y|; the weights of a vector's 8 samples are two
+// aligned 16-B reads from the window copy shifted by fs mod 4.  Returns F.
 #ifndef EXTRACT_R4_KV
 #define EXTRACT_R4_KV 9  // vectors per lane in one batch from L2 (a whole 1102-sample frame)
 #endif
-#ifndef EXTRACT_R4L_KV
-#define EXTRACT_R4L_KV 4  // the same from the LDS crop buffer (the next clip's loads are in flight)
-#endif
-#ifndef EXTRACT_R4F_KV
-#define EXTRACT_R4F_KV 5  // clip_fast's L2 fallback (a crop larger than the LDS buffer)
-#endif
-template <bool FROM_LDS, int KV = FROM_LDS ? EXTRACT_R4L_KV : EXTRACT_R4_KV>
 __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int L, int S,
-                                         int st, int en, const ClipStats &cs, int j0, int j1, int sb8, int wrank,
-                                         int lane, int vfix_lds = -1, short klast_lds = 0)
+                                         int st, int en, const ClipStats &cs, int j0, int j1, int wrank, int lane)
 {
     const int n = cur.n, lead = cur.lead;
     const int m = en - st;  // > 0 always (start < end)
@@ -800,14 +782,11 @@ __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, c
     const float sE = cs.invMf * cs.invMf, sM = cs.invMf;
     const int wrow = EXTRACT_WROW(L);
     const CanonX cx = canon_x(cs.mq, cs.t0);
-    // (L2) a 16-B load ending past the clip's last buffer vector drops a dword that straddles the
+    // a 16-B load ending past the clip's last buffer vector drops a dword that straddles the
     // descriptor's end (range checks are per dword): with an odd lead and a clip ending on a
     // vector boundary that dword holds the last sample, patched in from the aligned vector
-    // (LDS) the caller's: the crop DMA reads through the same descriptor, and the patch value is
-    // loaded before the next clip's loads are issued (a load here would wait for them)
-    const int vfix = FROM_LDS ? vfix_lds : ((lead & 1) && ((lead + n) & 7) == 0) ? (n - 1) >> 3 : -1;
-    const short klast = FROM_LDS ? klast_lds : vfix >= 0 ? load_vec(p, cur, cur.nvec - 1)[7] : (short)0;
-    const short8 *crop16 = reinterpret_cast<const short8 *>(c.crop);
+    const int vfix = ((lead & 1) && ((lead + n) & 7) == 0) ? (n - 1) >> 3 : -1;
+    const short klast = vfix >= 0 ? load_vec(p, cur, cur.nvec - 1)[7] : (short)0;
     auto frame_vec = [&](auto padded_t, auto near_t, const short8 &x8, const float *wr, int jb, int lim,
                          float2v &ea, float &m0, float &m1) {
         constexpr bool PADDED = decltype(padded_t)::value, NEAR0 = decltype(near_t)::value;
@@ -825,6 +804,7 @@ __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, c
             canon_pair(w, canon_x2<NEAR0>(x8[2 * h], x8[2 * h + 1], cx), ea, m0, m1);
         }
     };
+    constexpr int KV = EXTRACT_R4_KV;
     const int rl = lane & 15, row = lane >> 4;
     for (int gi = wrank; !(DSP_ABL & 1) && 4 * gi < F; gi += NWAVE) {
         const int g = 4 * gi + row;
@@ -845,12 +825,7 @@ __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, c
             const int vl = v0 + rl, vlim = vb - vl;
             short8 xv[KV];
 #pragma unroll
-            for (int k = 0; k < KV; k++) {
-                if constexpr (FROM_LDS)
-                    xv[k] = crop16[min(vl + 16 * k, vb) - sb8];
-                else
-                    xv[k] = load_cvec(p, cur, vl + 16 * k);
-            }
+            for (int k = 0; k < KV; k++) xv[k] = load_cvec(p, cur, vl + 16 * k);
             if (vfix >= 0)  // clip-uniform, rare
 #pragma unroll
                 for (int k = 0; k < KV; k++)
@@ -1283,7 +1258,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     STAMP(i, 4);
 
     // ---- R4: windowed frames over the crop [st, en) (r4_frames) --------------------------------
-    const int F = r4_frames<false>(p, c, cur, L, S, st, en, cs, sh->j0, sh->j1, 0, wid, lane);
+    const int F = r4_frames(p, c, cur, L, S, st, en, cs, sh->j0, sh->j1, wid, lane);
     STAMP(i, 12);
     if (!FAST && F > 128)
         for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
@@ -1378,147 +1353,31 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
 }
 
 // ==== FAST launches: clip_fast =================================================================
-// The clip's words stay in registers from R1 until the endpoint decisions are made; nothing of the
-// clip is re-read from memory:
-//   R1  registers: exact moments per word + sum / min / max; every word that holds a VAD frame
-//       end strictly inside it is also stored to that end's LDS slot (pass A reads it there)
-//   R2  registers: positive-sample bits
-//   VAD frames (LDS), p90 (wave 0) + noise (wave 1), scan (wave 0); thread 0 resolves the next clip
-//   crop: the words covering [st, en) are copied from the registers into the LDS crop buffer at the
-//       clip's own alignment; the registers are then dead and take the next clip's loads, in
-//       flight through R4, R5 and the loop turn
-//   R4  windowed crop frames from LDS;  R5 statistics
-// A crop larger than the buffer (no speech found, VAD off) takes R4 from L2, then the next loads.
-
+// Three 512-thread workgroups per CU (80 VGPRs), one clip at a time each; the clip's words are
+// loaded at its start and the two other workgroups on the CU cover the wait.  Round 5's A/B at
+// 100 000 clips (profiles/r05_ab.txt): 3.03 ms against 3.35 for two workgroups per CU with the next
+// clip's words prefetched during R5 -- more clips in flight per CU, not earlier loads, is what the
+// kernel needed.  Measured and not kept (same A/B): the crop copied into an LDS buffer after the
+// decisions so that R4 reads LDS and the registers take the next clip earlier -- from the
+// registers (16-way LDS bank conflicts on the copy) 3.78 ms, by LDS-DMA from L2 3.55 ms: R4 from LDS
+// took as long as from L2 (2.34 against 2.39 us per clip in the stamps; it is bound by its own
+// arithmetic), and the DMA's round trip sat on the critical path.
 #ifndef EXTRACT_FAST_PREFETCH
-#define EXTRACT_FAST_PREFETCH 1  // 0: each clip's loads are issued at its start (3 workgroups per CU)
-#endif
-#ifndef EXTRACT_CROP_DMA
-#define EXTRACT_CROP_DMA 1  // the crop into LDS by LDS-DMA from L2 (0: copied from the registers)
-#endif
-// floor(a / S) and a mod S (S >= 1, |a| < 2^20) by the float reciprocal and one correction step
-__device__ __forceinline__ int div_floor(int a, int S, float invS, int &m)
-{
-    int q = (int)floorf((float)a * invS);
-    m = a - q * S;
-    if (m >= S) {
-        m -= S;
-        q++;
-    } else if (m < 0) {
-        m += S;
-        q--;
-    }
-    return q;
-}
-// The VAD frame ends strictly inside buffer word w (S >= 32 and L >= 64: at most one frame start and
-// one frame end, never both ends of one frame): ts = 2f for the start of frame f, te = 2f + 1 for
-// its end (-1: none) -- exactly the frame ends vad_partial_word maps to word w.
-__device__ __forceinline__ void word_frame_ends(int w, int lead, int L, int S, float invS, int nv, int &ts, int &te)
-{
-    const int a = 32 * w - lead;  // clip sample of the word's first buffer sample (>= -7)
-    int m;
-    const int fs = div_floor(a, S, invS, m) + 1;  // the first frame start > a is fs S = a + S - m
-    ts = (m > S - 32 && fs < nv) ? 2 * fs : -1;
-    const int fe = div_floor(a - L, S, invS, m) + 1;  // the first frame end > a: fe S + L
-    te = (m > S - 32 && fe >= 0 && fe < nv) ? 2 * fe + 1 : -1;
-}
-__device__ __forceinline__ void store_slot(short8 *slots, int t, const short8 *q)
-{
-#pragma unroll
-    for (int k = 0; k < 4; k++) slots[4 * t + k] = q[k];
-}
-
-// VAD frames, FAST layout (nv <= 128 <= NT / 2): one lane pair per frame -- lane h of pair f owns
-// frame end t = 2f + h = tid and adds the exact moments of its partial word (from its LDS slot),
-// plus half of the interior word sums and of the sign changes.  Frame f = buffer samples [u0, u0 + L):
-// exact moments (wS1/wS2 words + the partial words at its ends), sign changes from the positive
-// bits -> c.vE / c.vZ.
-__device__ __forceinline__ void vad_frames_slots(const Ctx &c, const ClipRef &cur, int L, int S, const ClipStats &cs,
-                                                 int tid)
-{
-    const int nv = cs.nv, lead = cur.lead;
-    const int f = tid >> 1, lh = tid & 1;
-    const bool act = f < nv;
-    int s1 = 0;
-    unsigned long long s2 = 0;
-    int zc = 0;
-    if (act) {
-        int e0, e1;
-        const int pw = vad_partial_word(cur, L, S, nv, tid, e0, e1);
-        if (pw >= 0 && !(DSP_ABL & 8)) {
-            short8 qa[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) qa[k] = c.slots[4 * tid + k];
-            partial_moments(qa, e0, e1, s1, s2);
-        }
-        const int u0 = lead + f * S, u1 = u0 + L;
-        const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
-        const int wi0 = (u0 & 31) ? wa + 1 : wa, wi1 = (u1 & 31) ? wb - 1 : wb;
-        const int per = (wi1 - wi0 + 2) >> 1;
-        const int ws = wi0 + lh * per, we = min(ws + per - 1, wi1);
-#pragma unroll 4
-        for (int w = ws; w <= we; w++) {
-            s1 += c.wS1[w];
-            s2 += c.wS2[w];
-        }
-        const int np_ = L - 1, ph = (np_ + 1) >> 1;  // pairs [u0, u1 - 1) in halves
-        const int x0 = u0 + min(lh * ph, np_), x1 = u0 + min((lh + 1) * ph, np_);
-        zc = chg_run(c.posw, x0, x1);
-    }
-    s1 += dpp_i(s1, DPP_QXOR1);
-    {
-        const unsigned lo = dpp_i((int)(unsigned)s2, DPP_QXOR1), hi = dpp_i((int)(unsigned)(s2 >> 32), DPP_QXOR1);
-        s2 += ((unsigned long long)hi << 32) | lo;
-    }
-    zc += dpp_i(zc, DPP_QXOR1);
-    if (act && lh == 0) {
-        c.vE[f] = energy_from_moments(s2, s1, L, cs.t0, cs.mq - (double)cs.t0, cs.invM2);
-        c.vZ[f] = zc;
-    }
-}
-
-// one buffer word (32 samples, 16 dwords in q[0..3]) into the crop buffer at byte boff, the byte of
-// its first sample (boff = 0 mod 4 for an even lead, 2 mod 4 for an odd one: the sample pairs of
-// the crop buffer then straddle the word's dwords, realigned by v_alignbyte)
-__device__ __forceinline__ void crop_store_word(unsigned char *crop, const short8 *q, int boff, bool odd)
-{
-    uint32_t d[16];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const auto v = __builtin_bit_cast(uint4, q[k]);
-        d[4 * k] = v.x;
-        d[4 * k + 1] = v.y;
-        d[4 * k + 2] = v.z;
-        d[4 * k + 3] = v.w;
-    }
-    if (!odd) {
-        uint32_t *o = reinterpret_cast<uint32_t *>(crop + boff);
-#pragma unroll
-        for (int j = 0; j < 16; j++) o[j] = d[j];
-    } else {
-        *reinterpret_cast<uint16_t *>(crop + boff) = (uint16_t)d[0];
-        uint32_t *o = reinterpret_cast<uint32_t *>(crop + boff + 2);
-#pragma unroll
-        for (int j = 0; j < 15; j++) o[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], 2);
-        *reinterpret_cast<uint16_t *>(crop + boff + 62) = (uint16_t)(d[15] >> 16);
-    }
-}
+#define EXTRACT_FAST_PREFETCH 0  // 1: the next clip's words are loaded during R5 (two workgroups per
+#endif                           // CU: 128 VGPRs; at 80 they spill 64)
 
 // One clip, FAST layout, not the exact redo; its RREG words are already in flight into regs (word
 // r * NT + tid in regs[4r .. 4r+3]).  Endpoint energies from exact moments, decisions certified;
-// returns false on a near tie (the clip is redone by extract_exact_kernel; no next-clip loads were
-// issued), true when done (the next clip's loads -- sh->next, resolved before the crop -- are in
-// flight in regs).
+// returns false on a near tie (the clip is then redone by extract_exact_kernel).  Thread 0 resolves
+// the next clip (sh->next) before R4, also for a deferred clip.
 template <typename Resolve>
 __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, int i, const ClipRef &cur,
                                           short8 (&regs)[NRV], Resolve resolve)
 {
     Shared *sh = c.sh;
-#ifndef EXTRACT_FAST_OPAQUE
-#define EXTRACT_FAST_OPAQUE 1
-#endif
-    const int tid = EXTRACT_FAST_OPAQUE ? opaque_tid() : (int)threadIdx.x, lane = tid & 63,
-              wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // the thread index opaque: index arithmetic that depends only on it is recomputed where it is
+    // used, instead of being hoisted out of the persistent loop and held (spilled) across it
+    const int tid = opaque_tid(), lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     int L = p.L, S = p.S;
     asm volatile("" : "+s"(L), "+s"(S));  // per clip: constants derived from them are recomputed
     const int n = cur.n, lead = cur.lead, nword = cur.nword;
@@ -1532,27 +1391,13 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
         if (lane == 0) p.stamps[(size_t)i * 32 + 24 + wid] = __builtin_amdgcn_s_memtime();
     }
 #endif
-#if EXTRACT_SLOTS
-    const float invS = 1.0f / (float)S;
-    const int nv0 = (p.do_vad && n >= L) ? (n - L) / S + 1 : 0;  // = ClipStats::nv
-#endif
 
-    // ---- R1: integer sum / min / max; exact moments per word; the partial words of the frame ends
+    // ---- R1: integer sum / min / max; exact moments per 32-sample word --------------------------
     R1Acc acc = r1_acc_init();
 #pragma unroll
     for (int r = 0; r < RREG; r++) {
         const int w = r * NT + tid;
-        if (w < nword) {
-            r1_word(&regs[4 * r], w, nword, lead, n, acc, c.wS1, c.wS2);
-#if EXTRACT_SLOTS
-            if (nv0 > 0) {
-                int ts, te;
-                word_frame_ends(w, lead, L, S, invS, nv0, ts, te);
-                if (ts >= 0) store_slot(c.slots, ts, &regs[4 * r]);
-                if (te >= 0) store_slot(c.slots, te, &regs[4 * r]);
-            }
-#endif
-        }
+        if (w < nword) r1_word(&regs[4 * r], w, nword, lead, n, acc, c.wS1, c.wS2);
     }
     r1_reduce(acc, sh, wid, lane);
     __syncthreads();
@@ -1584,30 +1429,24 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
         if (w < nword) c.posw[w] = (DSP_ABL & 4) ? 0u : pos_word(&regs[4 * r], w, nword, lead, n, cs.tpos);
     }
     if (tid < 2) c.posw[nword + tid] = 0;
-#if !EXTRACT_SLOTS
     // the partial word of the frame end this thread sums in pass A (one frame end per thread),
     // re-read from L2 and issued before the barrier so that it is in flight while the workgroup
     // synchronises
     short8 qa[4];
     int pa_e0 = 0, pa_e1 = 0;
     const int pa_w = vad_partial_issue(p, cur, L, S, nv, tid, qa, pa_e0, pa_e1);
-#endif
     __syncthreads();
     STAMP(i, 2);
 
     // ---- R3: endpoint detection (:161-273) ------------------------------------------------
     if (nv > 0) {
-#if EXTRACT_SLOTS
-        vad_frames_slots(c, cur, L, S, cs, tid);
-#else
         vad_frames_fast(c, cur, L, S, cs, qa, pa_w, pa_e0, pa_e1, tid);
-#endif
         STAMP(i, 7);
         __syncthreads();
         STAMP(i, 8);
         if (wid == 0) {
             // the workgroup's critical path (p90, then the scan) runs on this one wave: it takes
-            // issue priority over the co-resident workgroup's waves until the decisions are made
+            // issue priority over the co-resident workgroups' waves until the decisions are made
             __builtin_amdgcn_s_setprio(2);
             p90_select_wave(c, nv, lane);
         }
@@ -1619,13 +1458,7 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
             if (lane == 0) sh->exact = cs.Mp > 0.0 ? flag : 0;
         }
     }
-    if (tid == 0) {  // claimed at the clip's start (-1: none); its load range for the prefetch below
-        const int nx = resolve();
-        const ClipRef nr = nx >= 0 ? clip_ref(p, nx) : clip_none();
-        sh->next = nx;
-        sh->nx_base = nr.base;
-        sh->nx_nvec = nr.nvec;
-    }
+    if (tid == 0) sh->next = resolve();  // claimed at the clip's start (-1: none)
     if (wid == 0) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
     int st = 0, en = n;
@@ -1643,81 +1476,13 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     }
     STAMP(i, 4);
 
-    // ---- the crop into LDS; the next clip's loads; R4 ---------------------------------------
-#if EXTRACT_CROP_DMA
-    // the crop's clip-relative vectors [st >> 3, (en - 1) >> 3] by LDS-DMA (buffer_load ... lds):
-    // 16-B loads at the clip's own alignment, each wave-instruction writing 1 KiB of LDS in lane
-    // order (no VGPRs, no LDS bank conflicts); crop vector v at LDS vector v - cv0.  They re-read
-    // the clip from L2; the clip's registers are dead here.
-    const int cv0 = st >> 3, cv1 = (en - 1) >> 3, sbase = 8 * cv0;
-    const bool in_lds = 16 * (cv1 - cv0 + 1) <= EXTRACT_CROP_BYTES;
-    // the last sample of a clip with an odd lead that ends on a vector boundary sits in a dword that
-    // straddles the descriptor's end, which a 16-B load drops: patched from the aligned vector
-    const int vfix = ((lead & 1) && ((lead + n) & 7) == 0) ? (n - 1) >> 3 : -1;
-    short klast = 0;
-#else
-    // the buffer words covering the crop's vectors [st >> 3, (en - 1) >> 3], copied whole from the
-    // registers: clip sample s at byte 2 (s - sbase), c0 = the first copied clip sample (>= -7),
-    // sbase = floor8(c0)
-    const int wf = ((st & ~7) + lead) >> 5, wl = (((en + 7) & ~7) - 1 + lead) >> 5;
-    const int c0 = 32 * wf - lead, sbase = (c0 >> 3) << 3;
-    const bool in_lds = 2 * (32 * (wl - wf + 1) + (c0 - sbase)) <= EXTRACT_CROP_BYTES;
-    const int vfix = -1;
-    const short klast = 0;
-#endif
-    int F = 0;
-    if (in_lds) {
-#if EXTRACT_CROP_DMA
-        const __amdgpu_buffer_rsrc_t rs = clip_rsrc(p, cur);
-        const int ncv = cv1 - cv0 + 1;
-        for (int j = 0; j * NT < ncv; j++) {  // wave-uniform trip count
-            const int v = cv0 + j * NT + tid;
-            if (v <= cv1)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rs, (__attribute__((address_space(3))) void *)(c.crop + 16 * (j * NT + 64 * wid)), 16,
-                    2 * lead + 16 * v, 0, 0, 0);
-        }
-        if (vfix >= 0) klast = load_vec(p, cur, cur.nvec - 1)[7];
-#else
-#pragma unroll
-        for (int r = 0; r < RREG; r++) {
-            const int w = r * NT + tid;
-            if (w >= wf && w <= wl) crop_store_word(c.crop, &regs[4 * r], 64 * w - 2 * lead - 2 * sbase, lead & 1);
-        }
-#endif
-        // keep the next clip's loads below the copy (a compiler memory barrier: LDS stores and
-        // buffer loads do not alias, so the loads could be hoisted above the copy)
-        asm volatile("" ::: "memory");
-        STAMP(i, 14);
-    } else {
-        F = r4_frames<false, EXTRACT_R4F_KV>(p, c, cur, L, S, st, en, cs, sh->j0, sh->j1, 0, wid, lane);
-        STAMP(i, 12);
-        __syncthreads();
-    }
-    if (EXTRACT_FAST_PREFETCH) {
-        // the clip's registers are dead in both paths: the next clip's loads, issued at ONE place
-        // (one register assignment for the loop-carried words, no copies at the back edge); the
-        // range comes from LDS (a load of offsets[] here would wait for the crop DMAs)
-        ClipRef nr = clip_none();
-        nr.base = uni_ll(sh->nx_base);
-        nr.nvec = uni(sh->nx_nvec);
-        issue_clip(regs, p, nr, opaque_tid());
-    }
-    if (in_lds) {
-#if EXTRACT_CROP_DMA
-        // this wave's crop DMAs (and the patch load) have landed -- the NRV next-clip loads issued
-        // after them stay in flight -- then every wave's: a raw barrier (__syncthreads() would wait
-        // for the next clip's loads too)
-        static_assert(NRV == 12, "the counted wait below leaves NRV loads in flight");
-        asm volatile("s_waitcnt vmcnt(12)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-#else
-        __syncthreads();
-#endif
-        STAMP(i, 15);
-        F = r4_frames<true>(p, c, cur, L, S, st, en, cs, sh->j0, sh->j1, sbase >> 3, wid, lane, vfix, klast);
-        STAMP(i, 12);
-        __syncthreads();
+    // ---- R4: windowed frames over the crop [st, en) (r4_frames) --------------------------------
+    const int F = r4_frames(p, c, cur, L, S, st, en, cs, sh->j0, sh->j1, wid, lane);
+    STAMP(i, 12);
+    __syncthreads();
+    if (EXTRACT_FAST_PREFETCH) {  // regs are dead: the next clip's words load while R5 runs
+        const int nx = sh->next;
+        issue_clip(regs, p, nx >= 0 ? clip_ref(p, nx) : clip_none(), opaque_tid());
     }
     STAMP(i, 5);
 
@@ -1774,8 +1539,6 @@ __device__ __forceinline__ Ctx ctx_from(const ExtractCarve &cv, unsigned char *l
     c.rank = reinterpret_cast<int *>(lds + cv.rank);
     c.pS1 = reinterpret_cast<int *>(lds + cv.pS1);
     c.pS2 = reinterpret_cast<unsigned long long *>(lds + cv.pS2);
-    c.slots = reinterpret_cast<short8 *>(lds + cv.slots);
-    c.crop = lds + cv.crop;
     c.ofeat = reinterpret_cast<float *>(lds + cv.ost);
     c.ose = reinterpret_cast<int32_t *>(lds + cv.ost + 4 * 15 * EXTRACT_OSTAGE);
     c.onf = c.ose + 2 * EXTRACT_OSTAGE;
@@ -1864,16 +1627,15 @@ __device__ __forceinline__ void flush_outputs(const ExtractParams &p, const Ctx 
 // measured 3.41 against 3.35 ms: it added 10% VALU and 49% SALU instructions, and was removed
 // (the A/B's raw record was not kept).
 
-// 128 VGPRs: two 512-thread workgroups per CU
-#ifndef EXTRACT_WAVES_PER_EU
-#define EXTRACT_WAVES_PER_EU 4
-#endif
+// registers: a 512-thread workgroup puts 2 waves on each SIMD, so W workgroups per CU allow
+// 512 / (2 W) VGPRs -- FAST 80 (three per CU), generic 128 (two per CU)
 
 // ---- one clip at a time per workgroup (both layouts) --------------------------------------------
 // A near tie (an endpoint decision within the certification margin) leaves the clip with status
 // DSP_CLIP_UNCERTIFIED; extract_exact_kernel, launched next on the stream, redoes it.
 template <bool FAST>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(EXTRACT_WAVES_PER_EU))) void extract_kernel(ExtractParams p)
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2 * (FAST ? EXTRACT_WG_PER_CU : EXTRACT_WG_PER_CU_GENERIC))))
+void extract_kernel(ExtractParams p)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     Ctx c = make_ctx<FAST>(p, lds);
@@ -2065,7 +1827,8 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     // launch fits it
     const bool fast = extract_fast_fits((int)max_len, frame_length, frame_shift);
     const size_t lds_launch = fast ? (size_t)extract_carve_fast().total : lds;
-    const int per_cu = std::max(1, std::min<int>(EXTRACT_WG_PER_CU, (int)(EXTRACT_LDS_LIMIT / lds_launch)));
+    const int per_cu = std::max(1, std::min<int>(fast ? EXTRACT_WG_PER_CU : EXTRACT_WG_PER_CU_GENERIC,
+                                                 (int)(EXTRACT_LDS_LIMIT / lds_launch)));
     const int slots = per_cu * num_cus;
     const int grid = B < slots ? B : slots;
     p.qchunk = B < 64 * (int64_t)grid ? 2 : 4;  // short batches: a finer tail

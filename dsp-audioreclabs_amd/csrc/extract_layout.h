@@ -1,12 +1,10 @@
 // LDS carve-up of the extraction kernel (host and device agree on it).
 //
 // The clip itself is NOT in LDS: it is held in registers (EXTRACT_RREG 32-sample words per
-// thread) from R1 until the endpoint decisions are made.  LDS holds per-word summaries (positive-
-// sample bits, exact moments), the window table and the small per-frame arrays.  The FAST layout
-// overlays the per-word moments and the partial words of the VAD frame ends (both dead once the
-// VAD frames are summed) with a crop buffer: after the decisions the crop is copied there from the
-// registers, so R4 reads LDS, not L2, and the registers take the next clip's loads (~78 KB per
-// workgroup, two workgroups per CU).  The generic layout re-reads the crop from L2.
+// thread) for the two passes that need every sample, and re-read from L2 by the phases that need
+// a few (crop frames, partial words at VAD frame edges).  LDS holds per-word summaries (positive-
+// sample bits, exact moments), the window table and the small per-frame arrays (~48 KB in the
+// compile-time layout), so three workgroups share a CU.
 #ifndef DSP_EXTRACT_LAYOUT_H
 #define DSP_EXTRACT_LAYOUT_H
 
@@ -17,7 +15,10 @@
 #define EXTRACT_RREG 3                   // 32-sample words per thread held in registers
 #endif
 #ifndef EXTRACT_WG_PER_CU
-#define EXTRACT_WG_PER_CU 2              // resident workgroups per CU the register budget allows
+#define EXTRACT_WG_PER_CU 3              // resident FAST workgroups per CU (80 VGPRs, <= 53 KB LDS each)
+#endif
+#ifndef EXTRACT_WG_PER_CU_GENERIC
+#define EXTRACT_WG_PER_CU_GENERIC 2      // the generic layout's kernel (128 VGPRs)
 #endif
 #define EXTRACT_LDS_LIMIT (160 * 1024)   // one CU
 #define EXTRACT_SHARED_BYTES 512         // sizeof(dsp::Shared) rounded up (static_assert'ed)
@@ -32,7 +33,6 @@
 struct ExtractCarve {
     int sh, wtab, posw, wS2, wS1, vE, vZ, fE, fM, fZ, rank, pS2, pS1, ost, total;
     int nvcap, fcap, nwmax;
-    int slots, crop, cropcap;  // FAST layout only (0 in the generic one): partial-word slots, crop buffer
 };
 
 // Region offsets from the capacities: nwmax 32-sample words (incl. the alignment lead), nvcap VAD
@@ -80,21 +80,13 @@ __host__ __device__ inline ExtractCarve extract_carve(int ncap, int L, int S)
 
 // The fast kernel's layout is fixed at compile time (every LDS address an immediate) and serves
 // every launch whose clips fit it: the whole clip in registers, <= 128 VAD and feature frames,
-// window rows of <= EXTRACT_FAST_WROW floats (frame_length <= 1256), frame_length >= 64 and
-// frame_shift >= 32 (a 32-sample word then holds at most one frame start and one frame end, never
-// both ends of one frame).
+// window rows of <= EXTRACT_FAST_WROW floats (frame_length <= 1256).
 #define EXTRACT_FAST_NV 128
 #define EXTRACT_FAST_NF 128
 #ifndef EXTRACT_FAST_WROW
 #define EXTRACT_FAST_WROW 1280
 #endif
-#ifndef EXTRACT_CROP_BYTES
-#define EXTRACT_CROP_BYTES (48 * 1024)  // crop buffer: 24 576 samples (0.56 s at 44.1 kHz)
-#endif
 #define EXTRACT_FAST_NWORD (EXTRACT_THREADS * EXTRACT_RREG)
-#ifndef EXTRACT_SLOTS
-#define EXTRACT_SLOTS 0  // 1: R1 stores each frame end's partial word to an LDS slot for pass A
-#endif                   // (A/B: 0 re-reads it from L2, issued before the R2 barrier)
 __host__ __device__ constexpr ExtractCarve extract_carve_fast()
 {
     ExtractCarve c{};
@@ -110,34 +102,26 @@ __host__ __device__ constexpr ExtractCarve extract_carve_fast()
     DSP_TAKE(sh, EXTRACT_SHARED_BYTES);
     DSP_TAKE(wtab, 16 * EXTRACT_FAST_WROW);
     DSP_TAKE(posw, 4 * (c.nwmax + 2));
+    DSP_TAKE(wS2, 8 * c.nwmax);
+    DSP_TAKE(wS1, 4 * c.nwmax);
     DSP_TAKE(vE, 8 * c.nvcap);
     DSP_TAKE(vZ, 4 * c.nvcap);
     DSP_TAKE(fE, 4 * c.fcap);
     DSP_TAKE(fM, 4 * c.fcap);
     DSP_TAKE(fZ, 4 * c.fcap);
     DSP_TAKE(ost, 4 * 19 * EXTRACT_OSTAGE);
-    c.rank = c.pS1 = c.pS2 = o;  // unused by the FAST layout
-    // union: {per-word moments, partial-word slots} (R1 .. VAD frames) / crop buffer (R4)
-    const int u = o;
-    c.crop = u;
-    DSP_TAKE(wS2, 8 * c.nwmax);
-    DSP_TAKE(wS1, 4 * c.nwmax);
-#if EXTRACT_SLOTS
-    DSP_TAKE(slots, 64 * 2 * c.nvcap);  // the 32-sample word of each partial VAD frame end (16-B aligned)
-#else
-    c.slots = o;  // (pass A re-reads the partial words from L2)
-#endif
-    c.cropcap = EXTRACT_CROP_BYTES;
-    if (o < u + c.cropcap) o = u + c.cropcap;
+    c.rank = c.pS1 = c.pS2 = o;  // unused by the FAST layout (<= 128 frames; pass A sums in registers)
 #undef DSP_TAKE
     c.total = o;
     return c;
 }
+static_assert(EXTRACT_WG_PER_CU * extract_carve_fast().total <= EXTRACT_LDS_LIMIT,
+              "the FAST layout must fit EXTRACT_WG_PER_CU workgroups per CU");
 __host__ __device__ inline bool extract_fast_fits(int ncap, int L, int S)
 {
     const ExtractCarve c = extract_carve(ncap, L, S);
     return (ncap + 7 + 31) / 32 <= EXTRACT_FAST_NWORD && c.nvcap <= EXTRACT_FAST_NV &&
-           c.fcap <= EXTRACT_FAST_NF && EXTRACT_WROW(L) <= EXTRACT_FAST_WROW && L >= 64 && S >= 32;
+           c.fcap <= EXTRACT_FAST_NF && EXTRACT_WROW(L) <= EXTRACT_FAST_WROW;
 }
 
 #endif
