@@ -736,7 +736,6 @@ __device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur
     unsigned long long s2 = 0;
     int zc = 0;
     if (act) {
-        if (pa_w >= 0 && !(DSP_ABL & 8)) partial_moments(qa, pa_e0, pa_e1, s1, s2);
         const int u0 = lead + f * S, u1 = u0 + L;
         const int wa = u0 >> 5, wb = (u1 - 1) >> 5;
         const int wi0 = (u0 & 31) ? wa + 1 : wa, wi1 = (u1 & 31) ? wb - 1 : wb;
@@ -750,6 +749,9 @@ __device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur
         const int np_ = L - 1, ph = (np_ + 1) >> 1;  // pairs [u0, u1 - 1) in halves
         const int x0 = u0 + min(lh * ph, np_), x1 = u0 + min((lh + 1) * ph, np_);
         zc = chg_run(c.posw, x0, x1);
+        // the partial word last: its load (issued before the R2 barrier) lands while the LDS
+        // sums above run
+        if (pa_w >= 0 && !(DSP_ABL & 8)) partial_moments(qa, pa_e0, pa_e1, s1, s2);
     }
     s1 += dpp_i(s1, DPP_QXOR1);
     {
@@ -1423,15 +1425,17 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     STAMP(i, 1);
 
     // ---- R2: positive-sample bits, one 32-bit word per 32 buffer samples ---------------------
+    // then the partial word of the frame end this thread sums in pass A (one frame end per thread),
+    // re-read from L2 and issued before the barrier so that it is in flight while the workgroup
+    // synchronises.  Issued earlier, with the clip's words still live, it costs spills whose
+    // reloads wait for it: at the end of R1 3.38 ms, before R2 3.18, after R2 2.82
+    // (profiles/r05h_ab.txt, r05i_ab.txt)
 #pragma unroll
     for (int r = 0; r < RREG; r++) {
         const int w = r * NT + tid;
         if (w < nword) c.posw[w] = (DSP_ABL & 4) ? 0u : pos_word(&regs[4 * r], w, nword, lead, n, cs.tpos);
     }
     if (tid < 2) c.posw[nword + tid] = 0;
-    // the partial word of the frame end this thread sums in pass A (one frame end per thread),
-    // re-read from L2 and issued before the barrier so that it is in flight while the workgroup
-    // synchronises
     short8 qa[4];
     int pa_e0 = 0, pa_e1 = 0;
     const int pa_w = vad_partial_issue(p, cur, L, S, nv, tid, qa, pa_e0, pa_e1);

@@ -944,22 +944,25 @@ struct KnnLayout {
     size_t ref32, q32, cand_d, cand_i, misc, pilot_d, seed0, seed, total;
     int DP, KC, nsplit;
     int rstride, nsample, nsplit_p;  // seeded thresholds (rstride > 0): sample rows j * rstride
-    int rstride0, nsample0;          // the pilot's own seed: a smaller sample (rows j * rstride0)
+    int rstride0, nsample0, nsplit_p0;  // the pilot's own seed: a smaller sample (rows j * rstride0)
     bool exp;  // expanded-form screening (a spare padded column holds |r|^2)
     bool hd;   // D > 32: chunked direct-form screen (knn_screen_hd)
     bool mfma; // expanded form on the matrix cores (knn_screen_mfma)
 };
 
 static constexpr int KNN_DMAX = 4096;
-// seeded thresholds: a pilot over ~KNN_SEED_SAMPLE strided rows when the set has >= KNN_SEED_MIN_NR,
-// itself seeded by a pre-pilot over ~KNN_SEED_SAMPLE0 rows (a pilot from +inf thresholds is all
-// list warm-up: 84 us of a 0.8 ms job at 12.5k x 100k for 4% of the pairs); the split model's
-// warm-up term after seeding (rows)
+// seeded thresholds: a pilot over ~KNN_SEED_SAMPLE strided rows when the set has >= KNN_SEED_MIN_NR.
+// A pre-pilot over ~KNN_SEED_SAMPLE0 rows can seed the pilot itself (0: none, the pilot starts
+// from +inf).  Round 5's sweep (profiles/r05_knn_pilot_sweep.txt, whole job at 12.5k / 100k
+// queries): 0:4096 0.783 / 4.41 ms, 256:2048 0.84 / 4.64-4.76, 256:4096 0.786-0.796 / 4.48,
+// 512:8192 0.783-0.792 / 4.47, 1024:16384 0.83-0.84 / 4.71: the seeded pilot is not cheaper (its time
+// is its tile loads of strided rows and the per-workgroup fixed costs, not list warm-up), and a looser
+// seed costs the main screen more than it saves.
 #ifndef KNN_SEED_SAMPLE
-#define KNN_SEED_SAMPLE 2048
+#define KNN_SEED_SAMPLE 4096
 #endif
 #ifndef KNN_SEED_SAMPLE0
-#define KNN_SEED_SAMPLE0 256
+#define KNN_SEED_SAMPLE0 0
 #endif
 #ifndef KNN_SEED_MIN_NR
 #define KNN_SEED_MIN_NR 32768
@@ -1055,12 +1058,19 @@ KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
     // screen over every rstride-th row (~KNN_SEED_SAMPLE rows) seeds each query's threshold
     l.rstride = l.rstride0 = 0;
     l.nsample = l.nsample0 = 0;
-    l.nsplit_p = 0;
+    l.nsplit_p = l.nsplit_p0 = 0;
     if (l.mfma && Nr >= KNN_SEED_MIN_NR) {
-        l.rstride = (int)std::max<int64_t>(2, Nr / KNN_SEED_SAMPLE);
+        int64_t samp = KNN_SEED_SAMPLE, samp0 = KNN_SEED_SAMPLE0;
+#ifdef DSP_KNN_DIAG  // diagnostic build only: pilot sample sizes (tools/r05_knn_pilot.sh)
+        if (const char *e = getenv("DSP_KNN_SAMPLE")) samp = std::max(64, atoi(e));
+        if (const char *e = getenv("DSP_KNN_SAMPLE0")) samp0 = std::max(0, atoi(e));
+#endif
+        l.rstride = (int)std::max<int64_t>(2, Nr / samp);
         l.nsample = (int)((Nr + l.rstride - 1) / l.rstride);
-        l.rstride0 = (int)std::max<int64_t>(2, Nr / KNN_SEED_SAMPLE0);
-        l.nsample0 = (int)((Nr + l.rstride0 - 1) / l.rstride0);
+        if (samp0 > 0) {
+            l.rstride0 = (int)std::max<int64_t>(2, Nr / samp0);
+            l.nsample0 = (int)((Nr + l.rstride0 - 1) / l.rstride0);
+        }
     }
 #ifdef DSP_KNN_DIAG  // diagnostic build only: seeding off (DSP_KNN_SEED=0)
     if (const char *e = getenv("DSP_KNN_SEED"))
@@ -1092,7 +1102,9 @@ KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
         const int64_t qblocks = (Nq + dsp::mq_qpb(l.KC) - 1) / dsp::mq_qpb(l.KC);
         l.nsplit_p = (int)std::max<int64_t>(1, std::min<int64_t>({(2 * device_cus() + qblocks - 1) / qblocks,
                                                                   (l.nsample + dsp::MQ_TR - 1) / dsp::MQ_TR, 64}));
-        l.pilot_d = o; o += al((size_t)l.nsplit_p * Nq * l.KC * 4);  // (the pre-pilot: one split)
+        // the pre-pilot: splits of >= 64 sample rows, at most the pilot's count
+        l.nsplit_p0 = (int)std::max<int64_t>(1, std::min<int64_t>(l.nsplit_p, l.nsample0 / 64));
+        l.pilot_d = o; o += al((size_t)l.nsplit_p * Nq * l.KC * 4);
         l.seed0 = o;   o += al((size_t)Nq * 4);
         l.seed = o;    o += al((size_t)Nq * 4);
     }
@@ -1249,11 +1261,15 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
                 default: hipLaunchKernelGGL((dsp::knn_seed<36>), gs, dim3(256), 0, s, pd, nsp, Nq, prev, out, scale); break;
                 }
             };
-            const dim3 gp0(qb, 1u), gp(qb, (unsigned)l.nsplit_p);
-            DSP_SCREEN_MQ_ALL(true, gp0, (int64_t)l.nsample0, 1, pd, (int *)nullptr, l.rstride0, (const float *)nullptr);
-            seeds(1, nullptr, seed0, 1.f);
-            DSP_SCREEN_MQ_ALL(true, gp, (int64_t)l.nsample, l.nsplit_p, pd, (int *)nullptr, l.rstride, (const float *)seed0);
-            seeds(l.nsplit_p, seed0, seedp, seed_scale);
+            const dim3 gp0(qb, (unsigned)l.nsplit_p0), gp(qb, (unsigned)l.nsplit_p);
+            if (l.rstride0) {
+                DSP_SCREEN_MQ_ALL(true, gp0, (int64_t)l.nsample0, l.nsplit_p0, pd, (int *)nullptr, l.rstride0,
+                                  (const float *)nullptr);
+                seeds(l.nsplit_p0, nullptr, seed0, 1.f);
+            }
+            DSP_SCREEN_MQ_ALL(true, gp, (int64_t)l.nsample, l.nsplit_p, pd, (int *)nullptr, l.rstride,
+                              (const float *)(l.rstride0 ? seed0 : nullptr));
+            seeds(l.nsplit_p, l.rstride0 ? seed0 : nullptr, seedp, seed_scale);
         }
         const dim3 g(qb, (unsigned)l.nsplit);
         DSP_SCREEN_MQ_ALL(false, g, Nr, l.nsplit, cd, ci, 1, (const float *)seedp);
