@@ -47,7 +47,7 @@ OUT_BYTES_PER_CLIP = 15 * 4 + 2 * 4 + 4 + 4  # feat f32[15] + start/end + n_fram
 LLC_BYTES = 256 << 20  # MI355X Infinity Cache
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -70,7 +70,7 @@ def parse():
                     help="configs[0] leg: 1024 / 512-sample frames")
     ap.add_argument("--check-launch", action="store_true",
                     help="start the ranks and report the world size the process group saw (no GPU work)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def free_port():
@@ -116,6 +116,72 @@ def timed_launches(fn, n, stream):
         b.record(stream)
     torch.cuda.synchronize()
     return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+
+def assemble_result(args, world, ranks_seen, rehearsal, backend_name, C, total_frames, elapsed_x, elapsed_g,
+                    kern_ms):
+    """The bench line (rank 0).  world > 1: ``value`` is the K steps of extraction + all-gather
+    (configs[3] as BASELINE defines it); ``value_extract_only`` the same steps without the exchange."""
+    N = 44100
+    L, S, vad = args.frame_length, args.frame_shift, not args.no_vad
+    K = args.steps
+    bytes_per_launch = C * (2 * N + OUT_BYTES_PER_CLIP)
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "dsp::extract_kernel", "kernel_avg_ms": round(kern_ms, 5),
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+            "per_unit": "2*44100 B in + 76 B out per clip"}
+    pmc = os.path.join(REPO, "profiles", "pmc_extract.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            pm = json.load(f)
+        key = "%d_%d_%d_%s_%d" % (C, L, S, args.window, int(vad))
+        if key in pm:
+            roof["traffic"] = pm[key]["hbm_bytes_per_launch"]
+            roof["traffic_source"] = pm[key]["source"]
+    elapsed = elapsed_g if elapsed_g is not None else elapsed_x
+    result = {
+        "metric": METRIC,
+        "value": round(total_frames / elapsed, 1),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "ranks_seen": ranks_seen,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / K * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded 1 s int16 utterances generated on the device: noise floor + "
+                "fricative burst + voiced segment)",
+        "config": {"workload": "north star / BASELINE configs[3] batch: %d x 1 s 44.1 kHz utterances "
+                               "sharded over %d GPU(s), %s window, E/M/ZCR + %s"
+                               % (args.clips, world, args.window, "double-threshold VAD" if vad else "no VAD"),
+                   "clips": args.clips, "clips_per_gpu": C, "samples_per_clip": N, "frame_length": L,
+                   "frame_shift": S, "window": args.window, "vad": vad, "input": "int16 PCM resident in HBM",
+                   "frames_per_step": round(total_frames / K, 1),
+                   "parallelism": ("dp%d (clips sharded; each step = extraction + one packed %s all-gather "
+                                   "of the per-clip results)" % (world, backend_name)) if world > 1 else
+                                  "dp1 (no collective)",
+                   "launch": ("python loop of the %d steps (extraction + all-gather)" % K) if world > 1 else
+                             ("hip graph of the %d steps" % K if not args.no_graph else "python loop")},
+        "roofline": roof,
+    }
+    if world > 1:
+        # the same K steps without the exchange (hip graph): what the kernel alone scales to
+        result["value_extract_only"] = round(total_frames / elapsed_x, 1)
+        result["ms_per_step_extract_only"] = round(elapsed_x / K * 1e3, 5)
+    if rehearsal:
+        result["rehearsal"] = True
+        result["backend"] = backend_name
+        result["physical_gpus"] = 1
+        result["note"] = ("rehearsal of the multi-rank code path: %d ranks share cuda:0 over %s; not a "
+                          "scaling measurement" % (world, backend_name))
+    elif world > 1:
+        result["backend"] = backend_name
+    return result
 
 
 def main():
@@ -260,62 +326,8 @@ def main():
 
     result = None
     if rank == 0:
-        bytes_per_launch = C * (2 * N + OUT_BYTES_PER_CLIP)
-        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "dsp::extract_kernel", "kernel_avg_ms": round(kern_ms, 5),
-                "algorithmic_bytes_per_launch": bytes_per_launch,
-                "per_unit": "2*44100 B in + 76 B out per clip"}
-        pmc = os.path.join(REPO, "profiles", "pmc_extract.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                pm = json.load(f)
-            key = "%d_%d_%d_%s_%d" % (C, L, S, args.window, int(vad))
-            if key in pm:
-                roof["traffic"] = pm[key]["hbm_bytes_per_launch"]
-                roof["traffic_source"] = pm[key]["source"]
-        elapsed = elapsed_g if elapsed_g is not None else elapsed_x
-        result = {
-            "metric": METRIC,
-            "value": round(total_frames / elapsed, 1),
-            "unit": "frames/s",
-            "n_gpus": world,
-            "ranks_seen": ranks_seen,
-            "steps": K,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / K * 1e3, 5),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "fp32",
-            "data": "synthetic (seeded 1 s int16 utterances generated on the device: noise floor + "
-                    "fricative burst + voiced segment)",
-            "config": {"workload": "north star / BASELINE configs[3] batch: %d x 1 s 44.1 kHz utterances "
-                                   "sharded over %d GPU(s), %s window, E/M/ZCR + %s"
-                                   % (args.clips, world, args.window, "double-threshold VAD" if vad else "no VAD"),
-                       "clips": args.clips, "clips_per_gpu": C, "samples_per_clip": N, "frame_length": L,
-                       "frame_shift": S, "window": args.window, "vad": vad, "input": "int16 PCM resident in HBM",
-                       "frames_per_step": round(total_frames / K, 1),
-                       "parallelism": ("dp%d (clips sharded; each step = extraction + one packed %s all-gather "
-                                       "of the per-clip results)" % (world, backend_name)) if world > 1 else
-                                      "dp1 (no collective)",
-                       "launch": ("python loop of the %d steps (extraction + all-gather)" % K) if world > 1 else
-                                 ("hip graph of the %d steps" % K if not args.no_graph else "python loop")},
-            "roofline": roof,
-        }
-        if world > 1:
-            # the same K steps without the exchange (hip graph): what the kernel alone scales to
-            result["value_extract_only"] = round(total_frames / elapsed_x, 1)
-            result["ms_per_step_extract_only"] = round(elapsed_x / K * 1e3, 5)
-        if rehearsal:
-            result["rehearsal"] = True
-            result["backend"] = backend_name
-            result["physical_gpus"] = 1
-            result["note"] = ("rehearsal of the multi-rank code path: %d ranks share cuda:0 over %s; not a "
-                              "scaling measurement" % (world, backend_name))
-        elif world > 1:
-            result["backend"] = backend_name
+        result = assemble_result(args, world, ranks_seen, rehearsal, backend_name, C, total_frames, elapsed_x,
+                                 elapsed_g, kern_ms)
         if ag is not None:
             result["allgather"] = ag
         if cfg0 is not None:

@@ -222,12 +222,12 @@ __device__ __forceinline__ void issue_word(short8 *q, const ExtractParams &p, co
 // immediate, so no vector instruction runs between the loads (a VGPR rewritten between them made
 // the compiler's vmcnt bookkeeping wait for the first loads to land)
 __device__ __forceinline__ void issue_clip(short8 (&regs)[NRV], const ExtractParams &p, const ClipRef &c,
-                                           int tid = (int)threadIdx.x)
+                                           int tid = (int)threadIdx.x, int r0 = 0, int r1 = RREG)
 {
     const __amdgpu_buffer_rsrc_t rs = clip_rsrc(p, c);
     const int voff = 64 * tid;
 #pragma unroll
-    for (int r = 0; r < RREG; r++)
+    for (int r = r0; r < r1; r++)
 #pragma unroll
         for (int k = 0; k < 4; k++)
             regs[4 * r + k] = __builtin_bit_cast(
@@ -1365,8 +1365,9 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
 // took as long as from L2 (2.34 against 2.39 us per clip in the stamps; it is bound by its own
 // arithmetic), and the DMA's round trip sat on the critical path.
 #ifndef EXTRACT_FAST_PREFETCH
-#define EXTRACT_FAST_PREFETCH 0  // 1: the next clip's words are loaded during R5 (two workgroups per
-#endif                           // CU: 128 VGPRs; at 80 they spill 64)
+#define EXTRACT_FAST_PREFETCH 0  // rows of the next clip's words loaded during R5 (the rest at its
+#endif                           // start): 1 row 3.52 ms, 2 rows 3.70 ms against 2.85 ms without, at
+                                 // 100k clips (spills; profiles/r05j_ab_prefetch_rows.txt)
 
 // One clip, FAST layout, not the exact redo; its RREG words are already in flight into regs (word
 // r * NT + tid in regs[4r .. 4r+3]).  Endpoint energies from exact moments, decisions certified;
@@ -1484,9 +1485,9 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     const int F = r4_frames(p, c, cur, L, S, st, en, cs, sh->j0, sh->j1, wid, lane);
     STAMP(i, 12);
     __syncthreads();
-    if (EXTRACT_FAST_PREFETCH) {  // regs are dead: the next clip's words load while R5 runs
+    if (EXTRACT_FAST_PREFETCH) {  // regs are dead: the next clip's first rows load while R5 runs
         const int nx = sh->next;
-        issue_clip(regs, p, nx >= 0 ? clip_ref(p, nx) : clip_none(), opaque_tid());
+        issue_clip(regs, p, nx >= 0 ? clip_ref(p, nx) : clip_none(), opaque_tid(), 0, EXTRACT_FAST_PREFETCH);
     }
     STAMP(i, 5);
 
@@ -1667,7 +1668,10 @@ void extract_kernel(ExtractParams p)
             write_bad_clip(p, i, opaque_tid());
             inflight = false;
         } else {
-            if (!inflight) issue_clip(regs, p, cur, opaque_tid());
+            if (!inflight)
+                issue_clip(regs, p, cur, opaque_tid());
+            else if (FAST && EXTRACT_FAST_PREFETCH < RREG)  // the rows not prefetched
+                issue_clip(regs, p, cur, opaque_tid(), EXTRACT_FAST_PREFETCH, RREG);
             unsigned cl = 0;
             if (tid == 0) cl = queue_begin(Q, sh);
             c.stamp_clip = i;
@@ -1683,7 +1687,7 @@ void extract_kernel(ExtractParams p)
                 p.status[i] = DSP_CLIP_UNCERTIFIED;
                 if (p.queue) __hip_atomic_fetch_add(p.queue + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            inflight = (FAST ? EXTRACT_FAST_PREFETCH : EXTRACT_PREFETCH) && done;
+            inflight = (FAST ? EXTRACT_FAST_PREFETCH > 0 : EXTRACT_PREFETCH) && done;
         }
         __syncthreads();  // LDS summaries are rewritten by the next clip; sh->next published
         const int prev = i;

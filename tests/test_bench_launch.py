@@ -31,3 +31,39 @@ def test_bench_refuses_world_size_mismatch():
                        timeout=300)
     assert r.returncode == 2
     assert "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_multirank_line_carries_both_values():
+    """N > 1: ``value`` is extraction + all-gather per step, ``value_extract_only`` the graph-replayed
+    extraction alone; N = 1 has only ``value``."""
+    m = _bench_module()
+    args = m.parse([])
+    args.steps, args.clips = 10, 100000
+    r2 = m.assemble_result(args, 2, 2, True, "gloo", 50000, 4.0e8, 0.02, 0.03, 1.4)
+    assert r2["value"] == round(4.0e8 / 0.03, 1) and r2["value_extract_only"] == round(4.0e8 / 0.02, 1)
+    assert r2["ms_per_step"] == 3.0 and r2["ms_per_step_extract_only"] == 2.0
+    assert r2["rehearsal"] is True and r2["backend"] == "gloo" and r2["n_gpus"] == 2
+    r1 = m.assemble_result(args, 1, 1, False, None, 100000, 4.0e8, 0.02, None, 2.8)
+    assert "value_extract_only" not in r1 and r1["value"] == round(4.0e8 / 0.02, 1)
+    assert r1["config"]["parallelism"].startswith("dp1")
+
+
+def test_committed_rehearsal_line():
+    """The committed 2-rank rehearsal (gloo, one GPU) carries both values."""
+    p = os.path.join(REPO, "profiles", "r05_multirank_rehearsal_bench.json")
+    if not os.path.exists(p):
+        import pytest
+        pytest.skip("no round-5 rehearsal record yet")
+    with open(p) as f:
+        d = json.loads([l for l in f.read().splitlines() if l.startswith("{")][-1])
+    assert d["rehearsal"] is True and d["n_gpus"] == 2 and d["ranks_seen"] == 2
+    assert d["value"] > 0 and d["value_extract_only"] >= d["value"] * 0.5
+    assert d["allgather"]["collectives"] == 1
