@@ -91,6 +91,14 @@ static constexpr int NRV = 4 * RREG;       // 16-B vectors per thread in registe
     } while (0)
 #endif
 
+#ifdef DSP_MARKS  // diagnostic assembly listings only (tools/phase_insts.py): region labels
+#define MARK(name) asm volatile(";@@ " #name)
+#else
+#define MARK(name) \
+    do {           \
+    } while (0)
+#endif
+
 // The kernels' only argument, a plain aggregate passed by value.
 struct ExtractParams {
     const int16_t *pcm;
@@ -589,6 +597,60 @@ __device__ __forceinline__ void r1_word(const short8 *q, int w, int nword, int l
     wS2[w] = s2;
     a.K += s1;
 }
+// R1 of the FAST layout: the interior words from the registers, every lane alike (r1_interior),
+// and the clip's two edge words -- whose samples outside the clip must not count -- by one wave,
+// a sample per lane re-read from L2 (r1_edges): on the owning lanes the per-sample branches of
+// r1_word's edge loop cost their waves ~300 instructions before the R1 barrier.
+__device__ __forceinline__ void r1_interior(const short8 *q, int w, R1Acc &a, int *wS1, unsigned long long *wS2)
+{
+    int s1 = 0;
+    unsigned long long s2 = 0;
+    const short2v ones = {1, 1};
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            const short2v d = half_pair(q[k], h);
+            a.pmin = __builtin_elementwise_min(a.pmin, d);
+            a.pmax = __builtin_elementwise_max(a.pmax, d);
+            s1 = __builtin_amdgcn_sdot2(d, ones, s1, false);
+            s2 += (unsigned)sq2(d);  // <= 2^31: unsigned
+        }
+    wS1[w] = s1;
+    wS2[w] = s2;
+    a.K += s1;
+}
+// lane l: sample l & 31 of the first word (l < 32) or of the last (l >= 32, clips of two words or
+// more); issued at R1's start, consumed (r1_edges) after the interior words
+__device__ __forceinline__ int r1_edge_issue(const ExtractParams &p, const ClipRef &cur, int lane)
+{
+    const int w = lane < 32 ? 0 : cur.nword - 1, u = 32 * w + (lane & 31);
+    const bool valid = (lane < 32 || cur.nword > 1) && u >= cur.lead && u < cur.lead + cur.n;
+    const int x = (short)__builtin_amdgcn_raw_buffer_load_b16(clip_rsrc(p, cur), valid ? 2 * u : 0x40000000, 0, 0);
+    return valid ? x : 0x7fffffff;  // the marker is outside int16
+}
+__device__ __forceinline__ void r1_edges(int xv, int nword, int lane, R1Acc &a, int *wS1, unsigned long long *wS2)
+{
+    const bool valid = xv != 0x7fffffff;
+    const int x = valid ? xv : 0;
+    if (valid) {
+        a.kmin = min(a.kmin, x);
+        a.kmax = max(a.kmax, x);
+    }
+    a.K += x;
+    // the two words' moments by LDS integer atomics (exact in any order); one wave's LDS
+    // operations execute in program order, so the zeroing lands first
+    const int w = lane < 32 ? 0 : nword - 1;
+    if ((lane & 31) == 0 && (lane == 0 || nword > 1)) {
+        wS1[w] = 0;
+        wS2[w] = 0;
+    }
+    if (valid) {
+        __hip_atomic_fetch_add(wS1 + w, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(wS2 + w, (unsigned long long)(unsigned)(x * x), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
 // the wave's R1 partials -> sh->red_*[wid] (every lane of the wave active)
 __device__ __forceinline__ void r1_reduce(const R1Acc &a, Shared *sh, int wid, int lane)
 {
@@ -773,7 +835,9 @@ __device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur
 // windowed frame, :329-331), E += y^2, M += |y|; the weights of a vector's 8 samples are two
 // aligned 16-B reads from the window copy shifted by fs mod 4.  Returns F.
 #ifndef EXTRACT_R4_KV
-#define EXTRACT_R4_KV 9  // vectors per lane in one batch from L2 (a whole 1102-sample frame)
+#define EXTRACT_R4_KV 7  // vectors per lane in one batch from L2: 7 (896 samples per row) leaves
+                         // the FAST kernel without VGPR spills; 9 (a whole 1102-sample frame)
+                         // 2.71 ms, 7 2.65 ms at 100k clips (profiles/r05s_ab_prefetch_kv.txt)
 #endif
 __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int L, int S,
                                          int st, int en, const ClipStats &cs, int j0, int j1, int wrank, int lane)
@@ -1396,12 +1460,15 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
 #endif
 
     // ---- R1: integer sum / min / max; exact moments per 32-sample word --------------------------
+    MARK(R1);
     R1Acc acc = r1_acc_init();
 #pragma unroll
     for (int r = 0; r < RREG; r++) {
         const int w = r * NT + tid;
-        if (w < nword) r1_word(&regs[4 * r], w, nword, lead, n, acc, c.wS1, c.wS2);
+        if (w < nword && w > 0 && w < nword - 1) r1_interior(&regs[4 * r], w, acc, c.wS1, c.wS2);
     }
+    if (wid == NWAVE - 1) r1_edges(r1_edge_issue(p, cur, lane), nword, lane, acc, c.wS1, c.wS2);
+    MARK(R1red);
     r1_reduce(acc, sh, wid, lane);
     __syncthreads();
     if (tid == 0 && sh->sclear) {  // the last flush's slots (every thread has read them by now)
@@ -1409,6 +1476,7 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
         sh->schunk = -1;
         sh->sclear = 0;
     }
+    MARK(stats);
     if (wid == 0) {  // the clip statistics once, shared through LDS
         const ClipStats c0 = clip_stats(sh, n, L, S, p.do_vad);
         if (lane == 0) sh->cs = {c0.mq, c0.Mp, c0.invM2, c0.invMf, c0.tpos, c0.t0, c0.nv};
@@ -1426,6 +1494,7 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     STAMP(i, 1);
 
     // ---- R2: positive-sample bits, one 32-bit word per 32 buffer samples ---------------------
+    MARK(R2);
     // then the partial word of the frame end this thread sums in pass A (one frame end per thread),
     // re-read from L2 and issued before the barrier so that it is in flight while the workgroup
     // synchronises.  Issued earlier, with the clip's words still live, it costs spills whose
@@ -1437,6 +1506,7 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
         if (w < nword) c.posw[w] = (DSP_ABL & 4) ? 0u : pos_word(&regs[4 * r], w, nword, lead, n, cs.tpos);
     }
     if (tid < 2) c.posw[nword + tid] = 0;
+    MARK(paissue);
     short8 qa[4];
     int pa_e0 = 0, pa_e1 = 0;
     const int pa_w = vad_partial_issue(p, cur, L, S, nv, tid, qa, pa_e0, pa_e1);
@@ -1444,11 +1514,13 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     STAMP(i, 2);
 
     // ---- R3: endpoint detection (:161-273) ------------------------------------------------
+    MARK(passAB);
     if (nv > 0) {
         vad_frames_fast(c, cur, L, S, cs, qa, pa_w, pa_e0, pa_e1, tid);
         STAMP(i, 7);
         __syncthreads();
         STAMP(i, 8);
+        MARK(p90);
         if (wid == 0) {
             // the workgroup's critical path (p90, then the scan) runs on this one wave: it takes
             // issue priority over the co-resident workgroups' waves until the decisions are made
@@ -1458,11 +1530,13 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
         if (wid == 1) vad_noise(c, nv, lane);  // beside wave 0's p90 selection
         __syncthreads();
         STAMP(i, 3);
+        MARK(scan);
         if (wid == 0) {
             const int flag = vad_scan<true, true>(p, c, nv, lane);
             if (lane == 0) sh->exact = cs.Mp > 0.0 ? flag : 0;
         }
     }
+    MARK(resolve);
     if (tid == 0) sh->next = resolve();  // claimed at the clip's start (-1: none)
     if (wid == 0) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
@@ -1482,6 +1556,7 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     STAMP(i, 4);
 
     // ---- R4: windowed frames over the crop [st, en) (r4_frames) --------------------------------
+    MARK(R4);
     const int F = r4_frames(p, c, cur, L, S, st, en, cs, sh->j0, sh->j1, wid, lane);
     STAMP(i, 12);
     __syncthreads();
@@ -1492,8 +1567,10 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     STAMP(i, 5);
 
     // ---- R5: 15-d statistics (compute_statistics x 3, fe.py:46-62) ------------------------
+    MARK(R5);
     r5_fast(c, F, featb, wid, lane);
     STAMP(i, 9);
+    MARK(tail);
     if (p.seq)
         for (int g = tid; g < F && g < p.ld_seq; g += NT) {
             float *o = p.seq + ((size_t)i * p.ld_seq + g) * 3;
