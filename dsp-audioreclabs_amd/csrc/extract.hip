@@ -117,7 +117,7 @@ struct ExtractParams {
     unsigned long long *stamps;  // diagnostic build only (else null)
     unsigned *queue;             // caller's clip-queue scratch (NULL: static split), zero at launch;
                                  // the last workgroup out zeroes it again
-    int qchunk;                  // clips per queue chunk (host: 4, or 2 for short batches)
+    int qchunk;                  // clips per queue chunk (host: 4, 2 for short batches, 0: static split)
     ExtractCarve cv;             // LDS layout, computed on the host (kernel arguments can be
                                  // re-read instead of being held in registers)
 };
@@ -147,6 +147,8 @@ struct Shared {
     int schunk;                        // ... of this chunk
     int sclear;                        // the staged slots were flushed: thread 0 clears smask after
                                        // the next barrier (flush_outputs reads it in every thread)
+    long long noff[2];                 // offsets[noff_for], offsets[noff_for + 1]: the next clip's,
+    int noff_for;                      // loaded during R5 (FAST; -1: none)
 };
 static_assert(sizeof(Shared) <= EXTRACT_SHARED_BYTES, "grow EXTRACT_SHARED_BYTES");
 static_assert((EXTRACT_OSTAGE & (EXTRACT_OSTAGE - 1)) == 0 && EXTRACT_OSTAGE <= 32, "chunk of 2^k <= 32 clips");
@@ -157,10 +159,10 @@ struct ClipRef {
     bool ok;
 };
 
-__device__ __forceinline__ ClipRef clip_ref(const ExtractParams &p, int i)
+__device__ __forceinline__ ClipRef clip_ref_at(const ExtractParams &p, int64_t o0, int64_t o1)
 {
     ClipRef c;
-    const int64_t o0 = p.offsets[i], nn = p.offsets[i + 1] - o0;
+    const int64_t nn = o1 - o0;
     c.ok = nn > 0 && nn <= p.ncap;
     c.n = c.ok ? (int)nn : 0;
     c.base = o0 & ~(int64_t)7;
@@ -168,6 +170,10 @@ __device__ __forceinline__ ClipRef clip_ref(const ExtractParams &p, int i)
     c.nvec = c.ok ? (c.lead + c.n + 7) >> 3 : 0;  // 0: loads of the clip read zeros
     c.nword = (c.lead + c.n + 31) >> 5;
     return c;
+}
+__device__ __forceinline__ ClipRef clip_ref(const ExtractParams &p, int i)
+{
+    return clip_ref_at(p, p.offsets[i], p.offsets[i + 1]);
 }
 __device__ __forceinline__ ClipRef clip_none()
 {
@@ -678,12 +684,36 @@ __device__ __forceinline__ uint32_t pos_byte(const short8 &val, short2v tt, bool
     const unsigned x23 = __builtin_amdgcn_perm(a3, a2, 0x07050301u) & 0x80808080u;
     return ~(((x01 * 0x00204081u) >> 28) | (((x23 * 0x00204081u) >> 28) << 4)) & 0xFFu;
 }
+// the same byte without 32-bit multiplies (quarter rate): each pair's (k - tpos) saturated, its
+// sign bits shifted to bit 0 of each half (v_pk_lshrrev_b16), the four pairs weighted (1, 2), (4, 8),
+// (16, 32), (64, 128) and summed by v_dot2_u32_u16 -- the byte of negative samples, inverted
+#ifndef EXTRACT_R2_DOT
+#define EXTRACT_R2_DOT 1
+#endif
+typedef unsigned short ushort2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t neg_byte_dot(const short8 &val, short2v tt)
+{
+    uint32_t b = 0;
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+        const ushort2v sb = __builtin_bit_cast(ushort2v, __builtin_elementwise_sub_sat(half_pair(val, h), tt)) >> 15;
+        const ushort2v wgt = {(unsigned short)(1u << (2 * h)), (unsigned short)(2u << (2 * h))};
+        b = __builtin_amdgcn_udot2(sb, wgt, b, false);
+    }
+    return b;
+}
 __device__ __forceinline__ uint32_t pos_word(const short8 *q, int w, int nword, int lead, int n, int tpos)
 {
     const bool tbig = tpos > 32767;
     const short2v tt = {(short)(tbig ? 32767 : tpos), (short)(tbig ? 32767 : tpos)};
-    uint32_t P = pos_byte(q[0], tt, tbig) | (pos_byte(q[1], tt, tbig) << 8) | (pos_byte(q[2], tt, tbig) << 16) |
-                 (pos_byte(q[3], tt, tbig) << 24);
+    uint32_t P;
+    if (EXTRACT_R2_DOT)
+        P = tbig ? 0u
+                 : ~(neg_byte_dot(q[0], tt) | (neg_byte_dot(q[1], tt) << 8) | (neg_byte_dot(q[2], tt) << 16) |
+                     (neg_byte_dot(q[3], tt) << 24));
+    else
+        P = pos_byte(q[0], tt, tbig) | (pos_byte(q[1], tt, tbig) << 8) | (pos_byte(q[2], tt, tbig) << 16) |
+            (pos_byte(q[3], tt, tbig) << 24);
     if (w == 0 || w == nword - 1) {  // real samples only
         const int lo_ = min(max(lead - 32 * w, 0), 32), hi_ = min(max(lead + n - 32 * w, 0), 32);
         const uint32_t mhi = hi_ >= 32 ? ~0u : ((1u << hi_) - 1u);
@@ -977,16 +1007,18 @@ __device__ __forceinline__ void r5_fast(const Ctx &c, int F, float *featb, int w
 }
 
 // Clip queue (ABI 3).  p.queue: the caller's zeroed 64-byte scratch, words 0-7 the claim counters
-// of eight ranges of clip chunks (p.qchunk consecutive clips each; range x = the chunks
-// [x nch / 8, (x + 1) nch / 8)), word 8 the count of workgroups done.  A workgroup claims chunks
-// from the range of the XCD it runs on (HW_REG_XCC_ID: placement is a performance matter only,
-// any id is correct), then from the others in turn once its own is exhausted: one atomic per chunk
-// instead of per clip, consecutive clips on one XCD -- their 76-B output rows share cache lines in
-// that XCD's L2 instead of leaving it as partial-line writes -- and fast workgroups take more
-// chunks (a static i, i + G, ... split ends on the slowest workgroup: 3.19-3.98 ms spread at
-// 100 000 clips).  The chunk is 4 clips, 2 for batches of fewer than 64 clips per workgroup
-// (12 500 clips: 0.506 -> 0.484 ms, a shorter tail; 100 000: 3.387 against 3.409 ms with 2;
-// profiles/r04x_queue_chunk_ab.txt).  p.queue == NULL: the static split.  Thread 0 only.
+// of eight ranges of clip chunks (p.qchunk consecutive clips each), word 8 the count of workgroups
+// done.  Workgroup b's first chunk is chunk b, taken without a claim; the chunks after the first G
+// ([G, nch)) form the eight ranges (range x = [G + x D / 8, G + (x + 1) D / 8), D = nch - G).  A
+// workgroup claims chunks from the range of the XCD it runs on (HW_REG_XCC_ID: placement is a
+// performance matter only, any id is correct), then from the others in turn once its own is
+// exhausted: one atomic per chunk instead of per clip, consecutive clips on one XCD -- their 76-B
+// output rows share cache lines in that XCD's L2 instead of leaving it as partial-line writes --
+// and fast workgroups take more chunks (a static i, i + G, ... split ends on the slowest
+// workgroup: 3.19-3.98 ms spread at 100 000 clips).  The chunk is 4 clips, 2 for batches of fewer
+// than 64 clips per workgroup (12 500 clips: 0.506 -> 0.484 ms, a shorter tail; 100 000: 3.387
+// against 3.409 ms with 2; profiles/r04x_queue_chunk_ab.txt).  p.qchunk == 0 (at most two clips
+// per workgroup) or p.queue == NULL: the static split, no claims.  Thread 0 only.
 #ifndef EXTRACT_XCD_RANGES
 #define EXTRACT_XCD_RANGES 8  // 1: one range for every workgroup (A/B)
 #endif
@@ -994,17 +1026,24 @@ static_assert(EXTRACT_XCD_RANGES >= 1 && EXTRACT_XCD_RANGES <= 8, "queue_ws hold
 struct ClipQueue {  // wave-uniform; the mutable state lives in Shared (thread 0 only)
     unsigned *q;
     int B, nch, xcd, ch;
+    int s0;  // chunks [0, s0) are the workgroups' first, one each (chunk blockIdx.x), without a claim
 };
 __device__ __forceinline__ ClipQueue queue_open(const ExtractParams &p, Shared *sh)
 {
     ClipQueue Q;
-    Q.q = p.queue;
+    Q.q = p.qchunk > 0 ? p.queue : nullptr;  // qchunk 0: the static split (short batches)
     Q.B = p.B;
-    Q.ch = p.qchunk;  // a power of two <= EXTRACT_OSTAGE (host), so chunks never straddle a stage group
+    Q.ch = max(p.qchunk, 1);  // a power of two <= EXTRACT_OSTAGE (host), so chunks never straddle a stage group
     Q.nch = (p.B + Q.ch - 1) / Q.ch;
+    Q.s0 = min(Q.nch, (int)gridDim.x);
     Q.xcd = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;  // HW_REG_XCC_ID[3:0]
     if (threadIdx.x == 0) {
-        sh->qnext = sh->qend = sh->qrange = 0;
+        // the first chunk is chunk blockIdx.x: no launch-time claim (768 workgroups on 8 counters
+        // serialised ~4.8 us of every workgroup's prologue)
+        const int b = (int)blockIdx.x;
+        sh->qnext = b < Q.nch ? b * Q.ch : 0;
+        sh->qend = b < Q.nch ? min(Q.B, b * Q.ch + Q.ch) : 0;
+        sh->qrange = 0;
         sh->qcursor = (int)blockIdx.x - (int)gridDim.x;
     }
     return Q;
@@ -1029,7 +1068,7 @@ __device__ __forceinline__ unsigned queue_begin(const ClipQueue &Q, Shared *sh)
         sh->cdir = nx;
         return 0;
     }
-    if (sh->qrange >= EXTRACT_XCD_RANGES) {  // every range exhausted
+    if (sh->qrange >= EXTRACT_XCD_RANGES || Q.s0 == Q.nch) {  // every range exhausted, or none
         sh->cdir = -1;
         return 0;
     }
@@ -1044,7 +1083,8 @@ __device__ __forceinline__ int queue_end(const ClipQueue &Q, Shared *sh, unsigne
     if (sh->cdir != -2) return sh->cdir;
     int y = sh->cy;
     for (;;) {
-        const unsigned c0 = (unsigned)(y * Q.nch / NR), c1 = (unsigned)((y + 1) * Q.nch / NR);
+        const int D = Q.nch - Q.s0;  // the claimed chunks [s0, nch), in NR ranges
+        const unsigned c0 = (unsigned)(Q.s0 + y * D / NR), c1 = (unsigned)(Q.s0 + (y + 1) * D / NR);
         if (c0 + ret < c1) {
             const int first = (int)(c0 + ret) * Q.ch;
             sh->qnext = first + 1;
@@ -1569,6 +1609,13 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     // ---- R5: 15-d statistics (compute_statistics x 3, fe.py:46-62) ------------------------
     MARK(R5);
     r5_fast(c, F, featb, wid, lane);
+    if (wid == NWAVE - 1) {
+        // idle in R5: the next clip's offsets to LDS, so that the loop top does not wait for a global
+        // load (nor, through the in-order vmcnt, for the flushed output stores before it)
+        const int nx = sh->next;
+        if (nx >= 0 && lane < 2) sh->noff[lane] = p.offsets[nx + lane];
+        if (lane == 0) sh->noff_for = nx;
+    }
     STAMP(i, 9);
     MARK(tail);
     if (p.seq)
@@ -1732,13 +1779,15 @@ void extract_kernel(ExtractParams p)
         sh->smask = 0;
         sh->schunk = -1;
         sh->sclear = 0;
+        sh->noff_for = -1;
     }
     __syncthreads();
     WG_CK(19);
     short8 regs[NRV];
     bool inflight = false;  // regs already hold clip i's loads (issued by the previous clip)
     for (int i = sh->next; i >= 0;) {
-        const ClipRef cur = clip_ref(p, i);
+        STAMP(i, 20);
+        const ClipRef cur = (FAST && sh->noff_for == i) ? clip_ref_at(p, sh->noff[0], sh->noff[1]) : clip_ref(p, i);
         if (!cur.ok) {
             __syncthreads();  // everyone has read sh->next (the ok path has barriers in its body)
             if (tid == 0) sh->next = queue_next(Q, sh);
@@ -1767,12 +1816,14 @@ void extract_kernel(ExtractParams p)
             inflight = (FAST ? EXTRACT_FAST_PREFETCH > 0 : EXTRACT_PREFETCH) && done;
         }
         __syncthreads();  // LDS summaries are rewritten by the next clip; sh->next published
+        STAMP(i, 14);
         const int prev = i;
         i = sh->next;
         if (i < 0 || (i ^ prev) >= EXTRACT_OSTAGE) {  // next clip in another chunk
             flush_outputs(p, c, prev, opaque_tid());  // (addresses computed here, not hoisted and spilled)
             if (tid == 0) sh->sclear = 1;
         }
+        STAMP(prev, 15);
     }
     if (tid == 0) queue_done(p);
     WG_STAMP(22);
@@ -1916,7 +1967,8 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
                                                  (int)(EXTRACT_LDS_LIMIT / lds_launch)));
     const int slots = per_cu * num_cus;
     const int grid = B < slots ? B : slots;
-    p.qchunk = B < 64 * (int64_t)grid ? 2 : 4;  // short batches: a finer tail
+    // short batches: a finer tail; at most two clips per workgroup: the static split (no claims)
+    p.qchunk = B <= 2 * (int64_t)grid ? 0 : B < 64 * (int64_t)grid ? 2 : 4;
     static_assert(EXTRACT_OSTAGE >= 4, "qchunk <= EXTRACT_OSTAGE");
     const hipStream_t s = (hipStream_t)stream;
     if (fast) {

@@ -21,10 +21,18 @@ print("clip us  p50 %.2f p90 %.2f | first round p50 %.2f (wg<%d %.2f, wg>=%d %.2
     np.median(tot), np.percentile(tot, 90), np.median(tot[:G]), G // 2, np.median(tot[:G // 2]), G // 2,
     np.median(tot[G // 2:G]), np.median(tot[G:]) if C > G else 0))
 names = {13: "R1 load wait", 1: "R1 stats", 2: "R2 pos", 7: "VAD pass A", 8: "VAD pass B", 3: "p90", 10: "noise+thr", 11: "scan",
-         4: "vad out", 14: "crop copy", 15: "issue+barrier", 12: "R4 frames", 5: "R4 barrier(+issue)", 9: "R5 jobs",
-         6: "R5 out"}
-# the crop stamps (14, 15) exist only for clips whose crop went to LDS
-seq = [0, 13, 1, 2, 7, 8, 3, 10, 11, 4] + ([14, 15] if (st[:, 14] > 0).any() else []) + [12, 5, 9, 6]
+         4: "vad out", 12: "R4 frames", 5: "R4 barrier(+issue)", 9: "R5 jobs", 6: "R5 out", 14: "end barrier",
+         15: "flush"}
+seq = [0, 13, 1, 2, 7, 8, 3, 10, 11, 4, 12, 5, 9, 6, 14, 15]
+# loop top of each clip (slot 20): offsets load, its loads issued, queue claim -> clip start (0)
+top = (st[:, 0] - st[:, 20]) / cyc
+print("  %-14s p50 %.2f  (loop top -> clip start)" % ("loop top", np.median(top)))
+# where the workgroups' time goes: prologue + the clips' spans (loop top -> flushed) against the
+# workgroup's duration (the same shader clock)
+span = (st[:, 15] - st[:, 20]) / cyc
+wg_ck = (ck1 - ck0) / cyc
+print("workgroup time: sum over workgroups %.0f us = prologue %.0f + clip spans %.0f + rest %.0f (per clip %.2f)" % (
+    wg_ck.sum(), pro.sum(), span.sum(), wg_ck.sum() - pro.sum() - span.sum(), (wg_ck.sum() - pro.sum() - span.sum()) / C))
 for a, b in zip(seq, seq[1:]):
     d = (st[:, b] - st[:, a]) / cyc
     print("  %-14s p50 %.2f  oldWG %.2f newWG %.2f" % (names[b], np.median(d), np.median(d[:G // 2]), np.median(d[G // 2:G])))
