@@ -24,12 +24,14 @@ CLIP_NO_FRAMES = 3
 CLIP_TOO_LONG = 4
 CLIP_UNCERTIFIED = 5  # reserved (never produced)
 CLIP_FLAG_VAD_EXACT = 0x100
-ABI_VERSION = 3  # include/dsp_audiorec.h DSP_ABI_VERSION this binding is typed for
+ABI_VERSION = 4  # include/dsp_audiorec.h DSP_ABI_VERSION this binding is typed for
 QUEUE_WS_BYTES = 64  # DSP_QUEUE_WS_BYTES
 
 EXPORTS = ("dsp_extract_lds_bytes", "dsp_extract_features", "dsp_extract_general_workspace_bytes",
            "dsp_extract_general", "dsp_knn_workspace_bytes", "dsp_knn_workspace_fallbacks_offset",
-           "dsp_knn_classify", "dsp_zscore_fit", "dsp_zscore_apply", "dsp_abi_version")
+           "dsp_knn_classify", "dsp_zscore_fit", "dsp_zscore_apply", "dsp_wav_scan", "dsp_wav_read",
+           "dsp_abi_version")
+DSP_WAV_OTHER, DSP_WAV_S16_MONO, DSP_WAV_U8_MONO = 0, 1, 2
 
 _lib = None
 
@@ -86,6 +88,11 @@ def load_library(path=LIB_PATH):
     L.dsp_zscore_fit.argtypes = [vp, i64, i32, vp, vp, vp]
     L.dsp_zscore_apply.restype = i32
     L.dsp_zscore_apply.argtypes = [vp, i64, i32, vp, vp, vp, vp]
+    if hasattr(L, "dsp_wav_scan"):  # (older A/B variants lack the reader)
+        L.dsp_wav_scan.restype = i32
+        L.dsp_wav_scan.argtypes = [vp, i64, i32, vp, vp, vp]
+        L.dsp_wav_read.restype = i32
+        L.dsp_wav_read.argtypes = [vp, i64, i32, vp, vp, vp, vp, vp]
     _lib = L
     return L
 

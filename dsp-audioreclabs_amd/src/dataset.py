@@ -4,13 +4,15 @@ configuration extracted from the same HBM-resident PCM.
 
 The reference decodes and processes one file per loop iteration for every configuration it
 evaluates (train_model.py:21-110 inside ablation_study.py:146-163, 230-247;
-experiments/run_experiments.py:78-111 once per window type).  Here a dataset is decoded once,
-in parallel threads (``load_wav_pcm`` is file I/O plus numpy, both of which release the GIL),
-packed into one int16 buffer with int64 offsets, uploaded once, and each configuration is one
-fused kernel launch over all clips (``FeatureExtractor``).  ``iter_device_batches`` is the
+experiments/run_experiments.py:78-111 once per window type).  Here a dataset is decoded once --
+the mono 8/16-bit PCM files by the library's native reader (dsp_wav_scan / dsp_wav_read: threads
+without the interpreter lock, samples written straight into one pinned int16 buffer at their
+packed offsets), every other file by the Python reader (``load_wav_pcm``) -- uploaded once, and
+each configuration is one fused kernel launch over all clips (``FeatureExtractor``).  ``iter_device_batches`` is the
 streaming form for file lists larger than host or device memory: batch k+1 is decoded and copied
 on a side stream while batch k is being processed.
 """
+import ctypes
 import os
 from concurrent.futures import ThreadPoolExecutor
 from glob import glob
@@ -58,14 +60,97 @@ def pack_clips(clips):
 
 
 def _upload(pcm, off, device, stream=None):
-    """Pinned staging + asynchronous copy on ``stream`` (current stream if None)."""
+    """Pinned staging + asynchronous copy on ``stream`` (current stream if None); ``pcm`` a numpy
+    array or an already pinned host tensor."""
     import torch
-    hp = torch.from_numpy(pcm).pin_memory()
+    hp = pcm if isinstance(pcm, torch.Tensor) and pcm.is_pinned() else torch.from_numpy(np.asarray(pcm)).pin_memory()
     ho = torch.from_numpy(off).pin_memory()
     if stream is None:
         return hp.to(device, non_blocking=True), ho.to(device, non_blocking=True), (hp, ho)
     with torch.cuda.stream(stream):
         return hp.to(device, non_blocking=True), ho.to(device, non_blocking=True), (hp, ho)
+
+
+def _native_reader():
+    """The library with the batch WAV reader, or None (an older A/B variant library)."""
+    from . import _hip
+    L = _hip.load_library()
+    return L if hasattr(L, "dsp_wav_scan") else None
+
+
+def _cpaths(paths):
+    return (ctypes.c_char_p * len(paths))(*[os.fsencode(p) for p in paths])
+
+
+def read_packed(paths, n_threads=None, pinned=True, native=True):
+    """A file list decoded and packed for one upload per sample type.
+
+    -> (kept, skipped, groups): ``kept`` the indices into ``paths`` of the decoded, non-empty files
+    in order; ``skipped`` [(path, reason)] (the reference skips what it cannot process,
+    run_experiments.py:109-111); ``groups`` [(pos, pcm, offsets)] -- int16 clips first, then the
+    int32 ones (16-bit stereo sums beyond int16) -- with ``pos`` the int64 positions in ``kept``,
+    ``pcm`` a host tensor [total + 8] (pinned when ``pinned``; the 8-sample tail keeps the last
+    clip's 16-B vectors inside the buffer) and ``offsets`` int64 [len(pos) + 1]."""
+    import torch
+    from . import _hip
+    n, nt = len(paths), _threads(n_threads)
+    kind, ns, doff = np.zeros(n, np.int32), np.zeros(n, np.int64), np.zeros(n, np.int64)
+    L = _native_reader() if native else None
+    if L is not None and n:
+        _hip.check(L.dsp_wav_scan(_cpaths(paths), n, nt, kind.ctypes.data, ns.ctypes.data, doff.ctypes.data),
+                   "dsp_wav_scan")
+    py = np.nonzero(kind == _hip.DSP_WAV_OTHER)[0].tolist()
+    dec = dict(zip(py, _decode([paths[i] for i in py], nt)))
+    kept, skipped, wide = [], [], []
+    for i in range(n):
+        if kind[i] != _hip.DSP_WAV_OTHER:
+            pcm, err, size = None, None, int(ns[i])
+        else:
+            pcm, err = dec[i]
+            size = 0 if pcm is None else pcm.size
+        if size == 0:
+            skipped.append((paths[i], err or "empty file"))
+            continue
+        kept.append(i)
+        wide.append(pcm is not None and pcm.dtype == np.int32)
+    groups = []
+    for w in (False, True):
+        pos = np.array([j for j, x in enumerate(wide) if x == w], dtype=np.int64)
+        if pos.size == 0:
+            continue
+        files = [kept[j] for j in pos]
+        lens = np.array([ns[i] if kind[i] else dec[i][0].size for i in files], dtype=np.int64)
+        off = np.zeros(len(files) + 1, dtype=np.int64)
+        off[1:] = np.cumsum(lens)
+        buf = torch.empty(int(off[-1]) + 8, dtype=torch.int32 if w else torch.int16, pin_memory=pinned)
+        hv = buf.numpy()
+        hv[int(off[-1]):] = 0
+        nat = [j for j, i in enumerate(files) if kind[i] != _hip.DSP_WAV_OTHER]
+        if nat:
+            sel = [files[j] for j in nat]
+            k2 = np.ascontiguousarray(kind[sel])
+            n2, d2, o2 = (np.ascontiguousarray(a) for a in (ns[sel], doff[sel], off[nat]))
+            _hip.check(L.dsp_wav_read(_cpaths([paths[i] for i in sel]), len(sel), nt, k2.ctypes.data, n2.ctypes.data,
+                                      d2.ctypes.data, o2.ctypes.data, buf.data_ptr()), "dsp_wav_read")
+            if (k2 == _hip.DSP_WAV_OTHER).any():  # a file changed since the scan: all through Python
+                return read_packed(paths, n_threads, pinned, native=False)
+        for j, i in enumerate(files):
+            if kind[i] == _hip.DSP_WAV_OTHER:
+                hv[off[j]:off[j + 1]] = dec[i][0]
+        groups.append((pos, buf, off))
+    return kept, skipped, groups
+
+
+def upload_groups(groups, device):
+    """read_packed's groups -> ([(pos, device pcm, device offsets, longest clip)], the pinned
+    host buffers, to be kept alive until the asynchronous copies have run)."""
+    import torch
+    parts, pinned = [], []
+    for pos, buf, off in groups:
+        ho = torch.from_numpy(off).pin_memory()
+        parts.append((pos, buf.to(device, non_blocking=True), ho.to(device, non_blocking=True), int(np.diff(off).max())))
+        pinned.append((buf, ho))
+    return parts, pinned
 
 
 def _threads(n_threads):
@@ -90,26 +175,12 @@ class PCMDataset:
         from . import _hip
         self.device = device or _hip.require_device()
         files, self.class_names = list_dataset(data_dir)
-        decoded = _decode([f for f, _ in files], _threads(n_threads))
-        clips, self.files, self.skipped = [], [], []
-        for (path, ci), (pcm, err) in zip(files, decoded):
-            if pcm is None or pcm.size == 0:
-                self.skipped.append((path, err or "empty file"))
-                continue
-            clips.append(pcm)
-            self.files.append((path, ci))
-        if not clips:
+        kept, self.skipped, groups = read_packed([f for f, _ in files], n_threads)
+        if not kept:
             raise ValueError("no readable WAV files under %s" % data_dir)
+        self.files = [files[i] for i in kept]
         self.labels = np.array([ci for _, ci in self.files], dtype=np.int64)
-        self.parts, self._pinned = [], []
-        for wide in (False, True):
-            idx = np.array([j for j, c in enumerate(clips) if (c.dtype == np.int32) == wide], dtype=np.int64)
-            if idx.size == 0:
-                continue
-            pcm, off = pack_clips([clips[j] for j in idx])
-            dp, do, pin = _upload(pcm, off, self.device)
-            self.parts.append((idx, dp, do, int(np.diff(off).max())))
-            self._pinned.append(pin)
+        self.parts, self._pinned = upload_groups(groups, self.device)
         self.max_len = max(p_[3] for p_ in self.parts)
 
     def _run(self, fx):
@@ -191,16 +262,21 @@ def iter_device_batches(paths, batch_clips, n_threads=None, device=None):
 
     def prepare(lo):
         idx = list(range(lo, min(lo + batch_clips, len(paths))))
-        dec = _decode([paths[i] for i in idx], nt)
-        keep = [(i, p) for i, (p, e) in zip(idx, dec) if p is not None and p.size > 0]
-        skipped = [(paths[i], e or "empty file") for i, (p, e) in zip(idx, dec) if p is None or p.size == 0]
-        if not keep:
+        kept, skipped, groups = read_packed([paths[i] for i in idx], nt)
+        if not kept:
             return None, [], skipped
-        pcm, off = pack_clips([p for _, p in keep])
+        if len(groups) == 1:
+            pcm, off = groups[0][1], groups[0][2]
+        else:  # int16 and int32 clips in one batch: one int32 buffer in file order
+            byp = {}
+            for pos, buf, goff in groups:
+                for j, q in enumerate(pos):
+                    byp[int(q)] = buf.numpy()[goff[j]:goff[j + 1]]
+            pcm, off = pack_clips([byp[q] for q in range(len(kept))])
         dp, do, pin = _upload(pcm, off, device, copy_stream)
         ev = torch.cuda.Event()
         ev.record(copy_stream)
-        return (dp, do, int(np.diff(off).max()), ev, pin), [i for i, _ in keep], skipped
+        return (dp, do, int(np.diff(off).max()), ev, pin), [idx[k] for k in kept], skipped
 
     try:
         fut = pool.submit(prepare, 0)

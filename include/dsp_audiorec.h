@@ -30,8 +30,9 @@
 extern "C" {
 #endif
 
-#define DSP_ABI_VERSION 3  /* 2: dsp_extract_features takes the clip-queue scratch (queue_ws);
-                              3: queue_ws is 64 bytes (per-XCD chunk counters) */
+#define DSP_ABI_VERSION 4  /* 2: dsp_extract_features takes the clip-queue scratch (queue_ws);
+                              3: queue_ws is 64 bytes (per-XCD chunk counters);
+                              4: the batch WAV reader (dsp_wav_scan / dsp_wav_read) */
 
 /* return codes */
 #define DSP_OK 0
@@ -63,12 +64,11 @@ extern "C" {
 size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int frame_shift);
 
 /*
- * dsp_extract_features -- fused per-clip pipeline: persistent workgroups (two per CU), each taking
- * one clip at a time from a clip queue, the clip held in registers until its endpoints are
- * decided; the crop is then copied into LDS and the registers take the next clip's loads while
- * the crop frames and statistics are computed.  A second launch on the same stream redoes
- * near-tie endpoint decisions on the bit-exact path (it returns at once when the first counted
- * none in queue_ws).
+ * dsp_extract_features -- fused per-clip pipeline: persistent workgroups (three per CU on the
+ * compile-time layout), each taking one clip at a time -- its first clip by its own index, the
+ * rest from a clip queue -- with the clip held in registers until its endpoints are decided and
+ * the crop's frames re-read from L2.  A second launch on the same stream redoes near-tie endpoint
+ * decisions on the bit-exact path (it returns at once when the first counted none in queue_ws).
  * Replaces, per clip, the chain
  *   preprocess            src/audio_processing.py:78-90   (remove_dc :49-59, normalize_audio :62-75)
  *   endpoint_detection    src/audio_processing.py:135-275 (when do_vad != 0)
@@ -182,6 +182,27 @@ int dsp_knn_classify(const double *ref, const int32_t *ref_labels, int64_t Nr, c
 int dsp_zscore_fit(const double *X, int64_t N, int D, double *mean, double *std, void *stream);
 int dsp_zscore_apply(const double *X, int64_t N, int D, const double *mean, const double *std,
                      double *out, void *stream);
+
+/*
+ * Batch WAV reader -- host only (no GPU, no stream): the file side of load_wav
+ * (src/audio_processing.py:9-46) for a whole file list, on n_threads native threads.
+ * dsp_wav_scan walks each file's RIFF chunks ('fmt ' with WAVE_FORMAT_PCM before 'data', chunks
+ * padded to even sizes, nframes = data bytes // frame bytes, the data fully present) and reports
+ * kind[i] = DSP_WAV_S16_MONO or DSP_WAV_U8_MONO with nsamp[i] samples at byte data_off[i], or
+ * DSP_WAV_OTHER (any other layout, stereo included, or an unreadable / malformed file: the
+ * caller's own reader decodes it or reports the reference's error).  dsp_wav_read writes the
+ * samples of every S16/U8 mono file with nsamp > 0 to dst + dst_off[i] (HOST memory, e.g. a pinned
+ * staging buffer): int16 as stored, 8-bit as ((u8 - 128) mod 256) like load_wav's uint8
+ * arithmetic (:31-34); a file that fails to read is turned into DSP_WAV_OTHER in kind[].
+ * paths: NUL-terminated file names.  Returns DSP_OK or DSP_ERR_ARGS.
+ */
+#define DSP_WAV_OTHER 0
+#define DSP_WAV_S16_MONO 1
+#define DSP_WAV_U8_MONO 2
+int dsp_wav_scan(const char *const *paths, int64_t n, int n_threads, int32_t *kind, int64_t *nsamp,
+                 int64_t *data_off);
+int dsp_wav_read(const char *const *paths, int64_t n, int n_threads, int32_t *kind, const int64_t *nsamp,
+                 const int64_t *data_off, const int64_t *dst_off, int16_t *dst);
 
 /* ABI version of the loaded library (DSP_ABI_VERSION). */
 int dsp_abi_version(void);

@@ -121,3 +121,62 @@ def test_riff_reader_equals_wave_module(tmp_path):
     x = np.frombuffer(pcm, np.int16)
     got, sr = load_wav_pcm(str(tmp_path / "mono16.wav"))
     assert sr == 44100 and got.dtype == np.int16 and np.array_equal(got, x)
+
+
+def test_native_wav_reader_equals_python_reader(tmp_path):
+    """The library's batch reader (dsp_wav_scan / dsp_wav_read, host only: no GPU) takes exactly
+    the mono 8/16-bit PCM files the RIFF walk takes and yields load_wav_pcm's samples for them;
+    everything else goes to the Python reader, so read_packed's kept files, skip reasons and
+    packed samples equal those of the pure-Python path (native=False)."""
+    from src import _hip
+    from src.audio_processing import load_wav_pcm
+    from src.dataset import read_packed
+    rng = np.random.default_rng(3)
+    pcm = rng.integers(-32768, 32768, 4001, dtype=np.int16).tobytes()
+    u8 = rng.integers(0, 256, 3333, dtype=np.uint8).tobytes()
+    cases = [
+        ("mono16", _riff([(b"fmt ", _fmt(1, 1, 44100, 16)), (b"data", pcm)])),
+        ("mono16_odd_bytes", _riff([(b"fmt ", _fmt(1, 1, 44100, 16)), (b"data", pcm[:1001])])),
+        ("mono8_odd_list", _riff([(b"fmt ", _fmt(1, 1, 8000, 8)), (b"LIST", b"abc"), (b"data", u8)])),
+        ("stereo16", _riff([(b"fmt ", _fmt(1, 2, 22050, 16)), (b"data", pcm)])),
+        ("stereo8", _riff([(b"fmt ", _fmt(1, 2, 8000, 8)), (b"data", u8[:3332])])),
+        ("fmt18", _riff([(b"fmt ", _fmt(1, 1, 44100, 16) + b"\0\0"), (b"data", pcm[:100])])),
+        ("float", _riff([(b"fmt ", _fmt(3, 1, 44100, 32)), (b"data", pcm[:400])])),
+        ("data_first", _riff([(b"data", pcm[:100]), (b"fmt ", _fmt(1, 1, 44100, 16))])),
+        ("truncated", _riff([(b"fmt ", _fmt(1, 1, 44100, 16)), (b"data", pcm)])[:-500]),
+        ("empty", _riff([(b"fmt ", _fmt(1, 1, 44100, 16)), (b"data", b"")])),
+        ("not_riff", b"RIFX" + b"\0" * 40),
+    ]
+    paths = []
+    for name, blob in cases * 3:  # repeated: several threads, chunks of 8 files
+        p = tmp_path / ("%s_%d.wav" % (name, len(paths)))
+        p.write_bytes(blob)
+        paths.append(str(p))
+    L = _hip.load_library()
+    n = len(paths)
+    kind, ns, off = np.zeros(n, np.int32), np.zeros(n, np.int64), np.zeros(n, np.int64)
+    from src.dataset import _cpaths
+    assert L.dsp_wav_scan(_cpaths(paths), n, 4, kind.ctypes.data, ns.ctypes.data, off.ctypes.data) == 0
+    native = {"mono16": 1, "mono16_odd_bytes": 1, "mono8_odd_list": 2, "fmt18": 1, "empty": 1}
+    for p, k, m in zip(paths, kind, ns):
+        name = p.rsplit("/", 1)[1].rsplit("_", 1)[0]
+        assert k == native.get(name, 0), name
+        if k:
+            assert m == load_wav_pcm(p)[0].size, name
+    a = read_packed(paths, 4, pinned=False)
+    b = read_packed(paths, 1, pinned=False, native=False)
+    assert a[0] == b[0] and a[1] == b[1]
+    assert len(a[2]) == len(b[2]) == 2  # int16 clips, then the int32 stereo sums
+    for (pa, ba, oa), (pb, bb, ob) in zip(a[2], b[2]):
+        assert np.array_equal(pa, pb) and np.array_equal(oa, ob) and torch_equal(ba, bb)
+    for q, i in enumerate(a[0]):  # every kept clip's samples equal load_wav_pcm's
+        for pos, buf, o in a[2]:
+            j = np.nonzero(pos == q)[0]
+            if j.size:
+                got = buf.numpy()[o[j[0]]:o[j[0] + 1]]
+                want = load_wav_pcm(paths[i])[0]
+                assert np.array_equal(got.astype(np.int64), want.astype(np.int64)), paths[i]
+
+
+def torch_equal(x, y):
+    return x.dtype == y.dtype and bool((x == y).all())

@@ -8,17 +8,19 @@ Three measurements, one JSON line:
 * ``user_wall_s``: ``python run.py --experiment classifier`` as a user starts it (a fresh process,
   interpreter start and every import included), timed from outside.
 * ``cold`` / ``warm``: the same ``run.main`` in a fresh instrumented process, twice.  The
-  instrumentation wraps the functions the run calls -- file listing, ``_decode``, ``pack_clips``,
-  ``_upload``, device initialisation, ``PCMDataset.extract`` (FeatureExtractor + fused launch +
+  instrumentation wraps the functions the run calls -- file listing, ``read_packed`` (the native
+  batch reader into one pinned buffer, the Python reader for any other file), ``upload_groups``,
+  device initialisation, ``PCMDataset.extract`` (FeatureExtractor + fused launch +
   device->host copy), ``train_test_split``, the z-score, each classifier's fit + evaluate, the
   result file -- and ``builtins.__import__`` (time spent importing modules, charged to the stage
   that triggered it).  ``unattributed_s`` = run.main's time minus every stage and every import
   outside a stage; ``imports_before_main_s`` is the process's import of the instrumented modules.
   The first pass pays the one-off costs (imports, HIP context, code-object loads); the second is
   the steady state.
-* ``decode``: ``src.dataset._decode`` alone over the same files -- files/s and MB/s -- with the
-  RIFF reader (``_read_wav``: one read, header walked in Python, ``np.frombuffer``) and with the
-  ``wave`` module, on 1 thread and on the default pool.
+* ``decode``: the decode stage alone over the same files -- files/s and MB/s -- for the native
+  reader (``read_packed``: dsp_wav_scan + dsp_wav_read into a pinned buffer) on the default thread
+  count and on 1 thread, and for the Python readers it replaced (``_decode``: the RIFF walk of
+  ``_read_wav`` and the ``wave`` module), 1 thread and the pool.
 
 Needs the GPU (extraction and KNN run there).
 
@@ -124,9 +126,8 @@ def instrumented(data, res):
     clock.imports_outside = 0.0
 
     ds.list_dataset = clock.wrap("list_files", ds.list_dataset)
-    ds._decode = clock.wrap("decode", ds._decode)
-    ds.pack_clips = clock.wrap("pack", ds.pack_clips)
-    ds._upload = clock.wrap("upload", ds._upload, sync=True)
+    ds.read_packed = clock.wrap("decode", ds.read_packed)
+    ds.upload_groups = clock.wrap("upload", ds.upload_groups, sync=True)
     hip.require_device = clock.wrap("device_init", hip.require_device)
     ds.PCMDataset.extract = clock.wrap("extraction", ds.PCMDataset.extract, sync=True)
     ms.train_test_split = clock.wrap("split", ms.train_test_split)
@@ -173,6 +174,16 @@ def decode_bench(data):
     paths = [f for f, _ in files]
     mb = sum(os.path.getsize(p) for p in paths) / 1e6
     out = {"files": len(paths), "MB": round(mb, 2), "pool_threads": ds._threads(None)}
+    for nt in (ds._threads(None), 1):
+        ds.read_packed(paths[:64], nt)
+        best = 1e9
+        for _ in range(3):
+            t = time.perf_counter()
+            kept, _, groups = ds.read_packed(paths, nt)
+            best = min(best, time.perf_counter() - t)
+        assert len(kept) == len(paths)
+        out["native_%dthr" % nt] = {"s": round(best, 4), "files_per_s": round(len(paths) / best, 1),
+                                    "MB_per_s": round(mb / best, 1), "includes": "scan + read into pinned buffer"}
     riff = ap._read_wav
     for reader in ("riff", "wave_module"):
         ap._read_wav = riff if reader == "riff" else (lambda f: ap._read_wav_module(f))
