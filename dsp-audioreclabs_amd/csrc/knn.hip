@@ -348,11 +348,120 @@ __global__ __launch_bounds__(64 * MQ_W) void knn_screen_mfma(const float *__rest
     }
 }
 
+// The pilot (seeded thresholds): over the sampled rows (sample row j = reference row j * rstride)
+// each query needs only an upper bound for the KC-th smallest distance of the whole set, and the
+// KC-th smallest of any KC distinct rows' distances is one.  So instead of top-KC lists (whose
+// insertions, from thresholds at +inf, were most of the old pilot's time) every lane keeps running
+// minima: lane (col, rg) of a 16 x 16 MFMA tile sees rows rb + 4 rg + v, v = 0..3, and keeps one
+// minimum per (v, step parity) -- PIL_CLS = 32 disjoint row classes per query and split, written
+// to pilot_d[split][query][32]; knn_seed then takes the KC-th smallest of all of them, which is
+// >= the KC-th smallest of the sample >= the KC-th smallest of the set.  Each class minimum over
+// ~nsample / 32 rows sits near quantile 1/(nsample/32) of the query's distances, and the 6th of 32
+// such near quantile 0.2 * 32 / nsample: as tight as the exact 6th smallest of the sample.
+static constexpr int PIL_CLS = 32;
+template <int DP>
+__global__ __launch_bounds__(64 * MQ_W) void knn_pilot_mfma(const float *__restrict__ ref32, int64_t Nr,
+                                                            const float *__restrict__ q32, int64_t Nq,
+                                                            int64_t self_offset, int nsplit,
+                                                            float *__restrict__ pilot_d, int rstride)
+{
+    constexpr int RS = mq_stride(DP), NJ = DP / 4, NV = DP / 16;
+    constexpr int MQ_T = KNN_MQ_T, MQ_QPB = 16 * MQ_T * MQ_W;
+    static_assert(MQ_TR % 32 == 0, "two 16-row steps per trip");
+    __shared__ __attribute__((aligned(16))) float tile[MQ_TR * RS];
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int col = lane & 15, rg = lane >> 4;
+    const int sp = blockIdx.y;
+    const int64_t per = (Nr + nsplit - 1) / nsplit;  // Nr: rows of the sample
+    const int64_t r0 = (int64_t)sp * per, r1 = min(Nr, r0 + per);
+    const int64_t wq0 = (int64_t)blockIdx.x * MQ_QPB + wid * MQ_T * 16;
+    const int64_t g0 = self_offset + wq0, g1 = g0 + 16 * MQ_T;
+    const int64_t slo = self_offset >= 0 ? (g0 + rstride - 1) / rstride : INT64_MIN / 2;
+    const int64_t shi = self_offset >= 0 ? (g1 + rstride - 1) / rstride : INT64_MIN / 2;
+    int64_t q[MQ_T], self[MQ_T];
+    float qb[MQ_T][NJ], qn[MQ_T], mn[MQ_T][2][4];
+#pragma unroll
+    for (int t = 0; t < MQ_T; t++) {
+        q[t] = wq0 + t * 16 + col;
+        const float *qr = q32 + (q[t] < Nq ? q[t] : 0) * DP;
+        float n = 0.f;  // |q|^2 as the screen computes it
+#pragma unroll
+        for (int c = 0; c < DP - 1; c++) n = fmaf(qr[c], qr[c], n);
+        qn[t] = n;
+#pragma unroll
+        for (int h = 0; h < NV; h++) {
+            const float4 v = *reinterpret_cast<const float4 *>(qr + 16 * h + 4 * rg);
+            qb[t][4 * h] = v.x;
+            qb[t][4 * h + 1] = v.y;
+            qb[t][4 * h + 2] = v.z;
+            qb[t][4 * h + 3] = v.w;
+        }
+        const int64_t sg = (self_offset >= 0 && q[t] < Nq) ? self_offset + q[t] : -1;
+        self[t] = (sg >= 0 && sg % rstride == 0) ? sg / rstride : -1;
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int v = 0; v < 4; v++) mn[t][h][v] = INFINITY;
+    }
+    for (int64_t t0 = r0; t0 < r1; t0 += MQ_TR) {
+        const int nt = (int)min((int64_t)MQ_TR, r1 - t0);
+        __syncthreads();
+        for (int e = tid; e < MQ_TR * DP / 4; e += 64 * MQ_W) {
+            const int row = e / (DP / 4), c4 = e % (DP / 4);
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (row < nt)
+                v = reinterpret_cast<const float4 *>(ref32 + (t0 + row) * rstride * DP)[c4];
+            else if (c4 == DP / 4 - 1)
+                v.w = INFINITY;  // |r|^2 of a padding row: distance +inf
+            *reinterpret_cast<float4 *>(tile + row * RS + 4 * c4) = v;
+        }
+        __syncthreads();
+        const int nt32 = (nt + 31) & ~31;
+        for (int s0 = 0; s0 < nt32; s0 += 32) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                float a[NJ];
+#pragma unroll
+                for (int u = 0; u < NV; u++) {
+                    const float4 v = *reinterpret_cast<const float4 *>(tile + (s0 + 16 * h + col) * RS + 16 * u + 4 * rg);
+                    a[4 * u] = v.x;
+                    a[4 * u + 1] = v.y;
+                    a[4 * u + 2] = v.z;
+                    a[4 * u + 3] = v.w;
+                }
+                mq_f4 acc[MQ_T];
+#pragma unroll
+                for (int t = 0; t < MQ_T; t++) acc[t] = mq_f4{qn[t], qn[t], qn[t], qn[t]};
+#pragma unroll
+                for (int j = 0; j < NJ; j++)
+#pragma unroll
+                    for (int t = 0; t < MQ_T; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], qb[t][j], acc[t], 0, 0, 0);
+                const int64_t rb = t0 + s0 + 16 * h;
+                if (rb < shi && rb + 16 > slo)  // wave-uniform: a query's own row may be here
+                    for (int t = 0; t < MQ_T; t++)
+                        for (int v = 0; v < 4; v++)
+                            if (rb + 4 * rg + v == self[t]) acc[t][v] = INFINITY;
+#pragma unroll
+                for (int t = 0; t < MQ_T; t++)
+#pragma unroll
+                    for (int v = 0; v < 4; v++) mn[t][h][v] = fminf(mn[t][h][v], acc[t][v]);
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < MQ_T; t++) {
+        if (q[t] >= Nq) continue;
+        float *o = pilot_d + ((size_t)sp * Nq + q[t]) * PIL_CLS + 8 * rg;
+        *reinterpret_cast<float4 *>(o) = make_float4(mn[t][0][0], mn[t][0][1], mn[t][0][2], mn[t][0][3]);
+        *reinterpret_cast<float4 *>(o + 4) = make_float4(mn[t][1][0], mn[t][1][1], mn[t][1][2], mn[t][1][3]);
+    }
+}
+
 // the seed of each query: the KC-th smallest of the pilot's nsplit x KC screened distances (the KC
 // smallest of the sample), one thread per query.  A pilot that was itself seeded (prev) kept only
 // distances below prev[q]: its KC-th is then either the sample's own KC-th (< prev) or +inf (the
 // sample's KC-th is >= prev), so the seed is the smaller of the two -- an upper bound either way.
-template <int KC>
+template <int KC, int NPER = KC>
 __global__ __launch_bounds__(256) void knn_seed(const float *__restrict__ cand_d, int nsplit, int64_t Nq,
                                                 const float *__restrict__ prev, float *__restrict__ seed,
                                                 float scale)
@@ -363,9 +472,9 @@ __global__ __launch_bounds__(256) void knn_seed(const float *__restrict__ cand_d
 #pragma unroll
     for (int i = 0; i < KC; i++) k32[i] = INFINITY;
     for (int s = 0; s < nsplit; s++) {
-        const float *c = cand_d + ((size_t)s * Nq + q) * KC;
+        const float *c = cand_d + ((size_t)s * Nq + q) * NPER;
 #pragma unroll
-        for (int i = 0; i < KC; i++) {
+        for (int i = 0; i < NPER; i++) {
             float v = c[i];
 #pragma unroll
             for (int j = 0; j < KC; j++) {
@@ -952,14 +1061,19 @@ struct KnnLayout {
 
 static constexpr int KNN_DMAX = 4096;
 // seeded thresholds: a pilot over ~KNN_SEED_SAMPLE strided rows when the set has >= KNN_SEED_MIN_NR.
-// A pre-pilot over ~KNN_SEED_SAMPLE0 rows can seed the pilot itself (0: none, the pilot starts
-// from +inf).  Round 5's sweep (profiles/r05_knn_pilot_sweep.txt, whole job at 12.5k / 100k
-// queries): 0:4096 0.783 / 4.41 ms, 256:2048 0.84 / 4.64-4.76, 256:4096 0.786-0.796 / 4.48,
-// 512:8192 0.783-0.792 / 4.47, 1024:16384 0.83-0.84 / 4.71: the seeded pilot is not cheaper (its time
-// is its tile loads of strided rows and the per-workgroup fixed costs, not list warm-up), and a looser
-// seed costs the main screen more than it saves.
+// Round 5: the pilot keeps class minima (knn_pilot_mfma) instead of top-KC lists -- at 4 096 rows
+// 84.8 -> 31.5 us at 12.5k queries, 409 -> 197 us at 100k, whole job 0.795-0.807 -> 0.738-0.757 ms
+// and 4.46-4.54 -> 4.27 ms (profiles/r05k2_knn_ab.txt) -- and the cheaper pilot affords a larger
+// sample: 2 048 / 4 096 / 8 192 / 16 384 rows 0.81-0.83 / 0.76 / 0.716-0.721 / 0.73-0.74 ms at 12.5k,
+// 4.45-4.48 / 4.27-4.30 / 4.15-4.20 / 4.30-4.34 ms at 100k (profiles/r05k2_pilot_sweep.txt).
+// A pre-pilot over ~KNN_SEED_SAMPLE0 rows can seed the list pilot (KNN_PILOT_MIN 0) itself (0:
+// none).  Round 5's sweep of the list pilot (profiles/r05_knn_pilot_sweep.txt): 0:4096 0.783 /
+// 4.41 ms, 256:4096 0.786-0.796 / 4.48, 512:8192 0.783-0.792 / 4.47: no gain.
+#ifndef KNN_PILOT_MIN
+#define KNN_PILOT_MIN 1  // the pilot keeps class minima (knn_pilot_mfma); 0: top-KC lists (A/B)
+#endif
 #ifndef KNN_SEED_SAMPLE
-#define KNN_SEED_SAMPLE 4096
+#define KNN_SEED_SAMPLE 8192
 #endif
 #ifndef KNN_SEED_SAMPLE0
 #define KNN_SEED_SAMPLE0 0
@@ -1104,7 +1218,7 @@ KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
                                                                   (l.nsample + dsp::MQ_TR - 1) / dsp::MQ_TR, 64}));
         // the pre-pilot: splits of >= 64 sample rows, at most the pilot's count
         l.nsplit_p0 = (int)std::max<int64_t>(1, std::min<int64_t>(l.nsplit_p, l.nsample0 / 64));
-        l.pilot_d = o; o += al((size_t)l.nsplit_p * Nq * l.KC * 4);
+        l.pilot_d = o; o += al((size_t)l.nsplit_p * Nq * std::max(l.KC, dsp::PIL_CLS) * 4);
         l.seed0 = o;   o += al((size_t)Nq * 4);
         l.seed = o;    o += al((size_t)Nq * 4);
     }
@@ -1262,6 +1376,25 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
                 }
             };
             const dim3 gp0(qb, (unsigned)l.nsplit_p0), gp(qb, (unsigned)l.nsplit_p);
+            if (KNN_PILOT_MIN) {
+                constexpr int pqpb = 16 * KNN_MQ_T * dsp::MQ_W;
+                const dim3 gpm((unsigned)((Nq + pqpb - 1) / pqpb), (unsigned)l.nsplit_p);
+                if (l.DP == 16)
+                    hipLaunchKernelGGL((dsp::knn_pilot_mfma<16>), gpm, b, 0, s, ref32, (int64_t)l.nsample, q32, Nq,
+                                       self_offset, l.nsplit_p, pd, l.rstride);
+                else
+                    hipLaunchKernelGGL((dsp::knn_pilot_mfma<32>), gpm, b, 0, s, ref32, (int64_t)l.nsample, q32, Nq,
+                                       self_offset, l.nsplit_p, pd, l.rstride);
+                switch (l.KC) {
+#define DSP_SEED_MIN(KCV)                                                                                   \
+    case KCV:                                                                                               \
+        hipLaunchKernelGGL((dsp::knn_seed<KCV, dsp::PIL_CLS>), gs, dim3(256), 0, s, pd, l.nsplit_p, Nq,       \
+                           (const float *)nullptr, seedp, seed_scale);                                        \
+        break
+                    DSP_SEED_MIN(6); DSP_SEED_MIN(8); DSP_SEED_MIN(16); DSP_SEED_MIN(24); DSP_SEED_MIN(36);
+#undef DSP_SEED_MIN
+                }
+            } else {
             if (l.rstride0) {
                 DSP_SCREEN_MQ_ALL(true, gp0, (int64_t)l.nsample0, l.nsplit_p0, pd, (int *)nullptr, l.rstride0,
                                   (const float *)nullptr);
@@ -1270,6 +1403,7 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
             DSP_SCREEN_MQ_ALL(true, gp, (int64_t)l.nsample, l.nsplit_p, pd, (int *)nullptr, l.rstride,
                               (const float *)(l.rstride0 ? seed0 : nullptr));
             seeds(l.nsplit_p, l.rstride0 ? seed0 : nullptr, seedp, seed_scale);
+            }
         }
         const dim3 g(qb, (unsigned)l.nsplit);
         DSP_SCREEN_MQ_ALL(false, g, Nr, l.nsplit, cd, ci, 1, (const float *)seedp);

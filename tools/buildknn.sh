@@ -6,4 +6,4 @@ cd "$(dirname "$0")/../dsp-audioreclabs_amd/csrc"
 n=$1; shift
 F="-O3 --offload-arch=gfx950 -std=c++17 -fPIC -I../../include -Wall -Wno-unused-function -mllvm -amdgpu-mfma-vgpr-form"
 /opt/rocm/bin/hipcc $F "$@" -c knn.hip -o ../lib/obj/knn_$n.o
-/opt/rocm/bin/hipcc $F -shared ../lib/obj/extract.o ../lib/obj/general.o ../lib/obj/knn_$n.o -o ../lib/libdsp_audiorec_$n.so
+/opt/rocm/bin/hipcc $F -shared ../lib/obj/extract.o ../lib/obj/general.o ../lib/obj/knn_$n.o ../lib/obj/wav_io.o -o ../lib/libdsp_audiorec_$n.so
