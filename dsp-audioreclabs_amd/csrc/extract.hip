@@ -1006,7 +1006,7 @@ __device__ __forceinline__ void r5_fast(const Ctx &c, int F, float *featb, int w
     }
 }
 
-// Clip queue (ABI 3).  p.queue: the caller's zeroed 64-byte scratch, words 0-7 the claim counters
+// Clip queue (ABI 5).  p.queue: the caller's zeroed 4 KiB scratch, words 0-7 the claim counters
 // of eight ranges of clip chunks (p.qchunk consecutive clips each), word 8 the count of workgroups
 // done.  Workgroup b's first chunk is chunk b, taken without a claim; the chunks after the first G
 // ([G, nch)) form the eight ranges (range x = [G + x D / 8, G + (x + 1) D / 8), D = nch - G).  A
@@ -1023,6 +1023,21 @@ __device__ __forceinline__ void r5_fast(const Ctx &c, int F, float *featb, int w
 #define EXTRACT_XCD_RANGES 8  // 1: one range for every workgroup (A/B)
 #endif
 static_assert(EXTRACT_XCD_RANGES >= 1 && EXTRACT_XCD_RANGES <= 8, "queue_ws holds 8 range counters");
+// queue_ws word w of the layout lives at word w * EXTRACT_QSTRIDE: every counter on its own 256-B
+// line.  Agent-scope atomics on one line serialise (across the eight XCDs they go past the L2s),
+// and with all eight counters in one 64-B line the claims of 768 workgroups queued behind each
+// other: at 12 500 clips the clips that claimed late in the launch took up to 85 us (p99 73 us).
+// One line per counter: 12.5k clips 0.454-0.459 -> 0.436-0.440 ms (span p99 73 -> 35 us, workgroups
+// p50 402 -> 363 us), 100k 2.634-2.656 -> 2.616-2.621 ms (profiles/r05qs_ab_queue_lines.txt,
+// r05qs_stamps.txt).  Probing the other ranges with loads before claiming: 2.75 ms at 100k.
+#ifndef EXTRACT_QSTRIDE
+#define EXTRACT_QSTRIDE 64
+#endif
+#ifndef EXTRACT_STEAL_PROBE
+#define EXTRACT_STEAL_PROBE 0  // 1: probe other ranges' counters with loads before claiming (A/B)
+#endif
+static_assert(11 * EXTRACT_QSTRIDE * 4 <= DSP_QUEUE_WS_BYTES, "queue_ws too small for the counter layout");
+__device__ __forceinline__ unsigned *qword(unsigned *q, int w) { return q + w * EXTRACT_QSTRIDE; }
 struct ClipQueue {  // wave-uniform; the mutable state lives in Shared (thread 0 only)
     unsigned *q;
     int B, nch, xcd, ch;
@@ -1075,7 +1090,7 @@ __device__ __forceinline__ unsigned queue_begin(const ClipQueue &Q, Shared *sh)
     const int y = (Q.xcd + sh->qrange) % EXTRACT_XCD_RANGES;
     sh->cy = y;
     sh->cdir = -2;
-    return __hip_atomic_fetch_add(Q.q + y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_fetch_add(qword(Q.q, y), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ int queue_end(const ClipQueue &Q, Shared *sh, unsigned ret)
 {
@@ -1092,10 +1107,19 @@ __device__ __forceinline__ int queue_end(const ClipQueue &Q, Shared *sh, unsigne
             return first;
         }
         // this range is used up: the next one (a blocking claim, rare: the end of the launch)
-        const int r = ++sh->qrange;
+        int r = ++sh->qrange;
+#if EXTRACT_STEAL_PROBE
+        // ranges whose counters already show every chunk claimed are skipped on a load, not a claim
+        for (; r < NR; r++) {
+            const int yy = (Q.xcd + r) % NR;
+            const unsigned v = __hip_atomic_load(qword(Q.q, yy), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((unsigned)(Q.s0 + yy * D / NR) + v < (unsigned)(Q.s0 + (yy + 1) * D / NR)) break;
+        }
+        sh->qrange = r;
+#endif
         if (r >= NR) return -1;
         y = (Q.xcd + r) % NR;
-        ret = __hip_atomic_fetch_add(Q.q + y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ret = __hip_atomic_fetch_add(qword(Q.q, y), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 __device__ __forceinline__ int queue_next(const ClipQueue &Q, Shared *sh) { return queue_end(Q, sh, queue_begin(Q, sh)); }
@@ -1104,11 +1128,11 @@ __device__ __forceinline__ int queue_next(const ClipQueue &Q, Shared *sh) { retu
 __device__ __forceinline__ void queue_done(const ExtractParams &p)
 {
     if (!p.queue) return;
-    const unsigned d = __hip_atomic_fetch_add(p.queue + 8, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned d = __hip_atomic_fetch_add(qword(p.queue, 8), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (d == gridDim.x - 1) {
 #pragma unroll
-        for (int y = 0; y < 8; y++) __hip_atomic_store(p.queue + y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(p.queue + 8, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        for (int y = 0; y < 8; y++) __hip_atomic_store(qword(p.queue, y), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(qword(p.queue, 8), 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1461,9 +1485,10 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
 // ==== FAST launches: clip_fast =================================================================
 // Three 512-thread workgroups per CU (80 VGPRs), one clip at a time each; the clip's words are
 // loaded at its start and the two other workgroups on the CU cover the wait.  Round 5's A/B at
-// 100 000 clips (profiles/r05_ab.txt): 3.03 ms against 3.35 for two workgroups per CU with the next
-// clip's words prefetched during R5 -- more clips in flight per CU, not earlier loads, is what the
-// kernel needed.  Measured and not kept (same A/B): the crop copied into an LDS buffer after the
+// 100 000 clips (profiles/r05e_ab_variants.txt): 3.04 ms against 3.36 for two workgroups per CU with
+// the next clip's words prefetched during R5 -- more clips in flight per CU, not earlier loads, is
+// what the kernel needed (2.64 ms after the R4, edge-word and compiler changes).
+// Measured and not kept (profiles/r05c_ab_crop.txt, r05d_ab_crop.txt): the crop copied into an LDS buffer after the
 // decisions so that R4 reads LDS and the registers take the next clip earlier -- from the
 // registers (16-way LDS bank conflicts on the copy) 3.78 ms, by LDS-DMA from L2 3.55 ms: R4 from LDS
 // took as long as from L2 (2.34 against 2.39 us per clip in the stamps; it is bound by its own
@@ -1787,6 +1812,9 @@ void extract_kernel(ExtractParams p)
     bool inflight = false;  // regs already hold clip i's loads (issued by the previous clip)
     for (int i = sh->next; i >= 0;) {
         STAMP(i, 20);
+#ifdef DSP_STAMPS
+        if (threadIdx.x == 0 && p.stamps) p.stamps[(size_t)i * 32 + 21] = blockIdx.x;  // the clip's workgroup
+#endif
         const ClipRef cur = (FAST && sh->noff_for == i) ? clip_ref_at(p, sh->noff[0], sh->noff[1]) : clip_ref(p, i);
         if (!cur.ok) {
             __syncthreads();  // everyone has read sh->next (the ok path has barriers in its body)
@@ -1811,7 +1839,7 @@ void extract_kernel(ExtractParams p)
             }
             if (!done && tid == 0) {
                 p.status[i] = DSP_CLIP_UNCERTIFIED;
-                if (p.queue) __hip_atomic_fetch_add(p.queue + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (p.queue) __hip_atomic_fetch_add(qword(p.queue, 9), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             inflight = (FAST ? EXTRACT_FAST_PREFETCH > 0 : EXTRACT_PREFETCH) && done;
         }
@@ -1837,7 +1865,7 @@ void extract_kernel(ExtractParams p)
 template <bool FAST>
 __global__ __launch_bounds__(NT) void extract_exact_kernel(ExtractParams p)
 {
-    if (p.queue && __hip_atomic_load(p.queue + 9, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+    if (p.queue && __hip_atomic_load(qword(p.queue, 9), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     Ctx c = make_ctx<FAST>(p, lds);
     Shared *sh = c.sh;
@@ -1869,10 +1897,10 @@ __global__ __launch_bounds__(NT) void extract_exact_kernel(ExtractParams p)
         }
     }
     if (p.queue && tid == 0) {  // every workgroup has read word 9 before its increment of word 10
-        const unsigned d = __hip_atomic_fetch_add(p.queue + 10, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned d = __hip_atomic_fetch_add(qword(p.queue, 10), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         if (d == gridDim.x - 1) {
-            __hip_atomic_store(p.queue + 9, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(p.queue + 10, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(qword(p.queue, 9), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(qword(p.queue, 10), 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }

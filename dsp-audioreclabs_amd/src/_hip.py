@@ -24,8 +24,8 @@ CLIP_NO_FRAMES = 3
 CLIP_TOO_LONG = 4
 CLIP_UNCERTIFIED = 5  # reserved (never produced)
 CLIP_FLAG_VAD_EXACT = 0x100
-ABI_VERSION = 4  # include/dsp_audiorec.h DSP_ABI_VERSION this binding is typed for
-QUEUE_WS_BYTES = 64  # DSP_QUEUE_WS_BYTES
+ABI_VERSION = 5  # include/dsp_audiorec.h DSP_ABI_VERSION this binding is typed for
+QUEUE_WS_BYTES = 4096  # DSP_QUEUE_WS_BYTES
 
 EXPORTS = ("dsp_extract_lds_bytes", "dsp_extract_features", "dsp_extract_general_workspace_bytes",
            "dsp_extract_general", "dsp_knn_workspace_bytes", "dsp_knn_workspace_fallbacks_offset",
@@ -61,7 +61,7 @@ def load_library(path=LIB_PATH):
     L.dsp_abi_version.restype = i32
     L.dsp_abi_version.argtypes = []
     # DSP_ABI_ANY=1: A/B tools loading an older variant library (tools/ab_bench.sh); the queue
-    # scratch this binding passes (64 zero bytes) serves ABI 2's 8-byte counter pair too
+    # scratch this binding passes (4 KiB of zeros) serves the older layouts (8 or 64 bytes) too
     if L.dsp_abi_version() != ABI_VERSION and not (os.environ.get("DSP_ABI_ANY") == "1" and L.dsp_abi_version() >= 2):
         raise HipError("%s has ABI %d, this binding expects %d: rebuild it" % (path, L.dsp_abi_version(), ABI_VERSION))
     missing = [e for e in EXPORTS if not hasattr(L, e)]

@@ -30,9 +30,10 @@
 extern "C" {
 #endif
 
-#define DSP_ABI_VERSION 4  /* 2: dsp_extract_features takes the clip-queue scratch (queue_ws);
+#define DSP_ABI_VERSION 5  /* 2: dsp_extract_features takes the clip-queue scratch (queue_ws);
                               3: queue_ws is 64 bytes (per-XCD chunk counters);
-                              4: the batch WAV reader (dsp_wav_scan / dsp_wav_read) */
+                              4: the batch WAV reader (dsp_wav_scan / dsp_wav_read);
+                              5: queue_ws is 4 KiB (each counter on its own 256-B line) */
 
 /* return codes */
 #define DSP_OK 0
@@ -41,7 +42,7 @@ extern "C" {
 #define DSP_ERR_WORKSPACE 3   /* workspace too small */
 #define DSP_ERR_HIP 1000      /* + hipError_t of the failed launch */
 
-#define DSP_QUEUE_WS_BYTES 64  /* dsp_extract_features' queue_ws */
+#define DSP_QUEUE_WS_BYTES 4096  /* dsp_extract_features' queue_ws */
 
 /* per-clip status[b] (low byte) -- same codes as the oracle */
 #define DSP_CLIP_OK 0
@@ -96,7 +97,7 @@ size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int frame_shift)
  * seq       (optional, may be NULL): float32 [B, ld_seq, 3] per-frame (E, M, ZCR) -- the
  *           'sequence' method of extract_features_from_frames (:114-129); frames beyond
  *           ld_seq are dropped.
- * queue_ws  (optional, may be NULL): DSP_QUEUE_WS_BYTES (64) bytes of device scratch, zero
+ * queue_ws  (optional, may be NULL): DSP_QUEUE_WS_BYTES (4096) bytes of device scratch, zero
  *           before the launch: the counters of the dynamic clip queue (persistent workgroups
  *           claim chunks of consecutive clips, from their own XCD's share first, so fast
  *           workgroups take more clips); the launch leaves it zero again, so it can be reused by

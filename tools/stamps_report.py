@@ -44,3 +44,22 @@ if (st[:, 24:32] > 0).all(axis=1).any():
     lw = (st[ok, 24:32] - st[ok, 0:1]) / cyc
     print("per-wave load landed after clip start us: median of max %.2f, median of min %.2f, per wave p50 %s" % (
         np.median(lw.max(1)), np.median(lw.min(1)), " ".join("%.2f" % v for v in np.median(lw, 0))))
+
+# clip spans by the clip's ordinal in its workgroup (slot 21: the workgroup, diagnostic build) and
+# the spread of the workgroups' clip counts
+wg = st[:, 21].astype(np.int64)
+if (st[:, 20] > 0).all() and wg.max() > 0:
+    order = np.lexsort((st[:, 20], wg))
+    ordinal = np.zeros(C, np.int64)
+    w_sorted = wg[order]
+    starts = np.r_[0, np.nonzero(np.diff(w_sorted))[0] + 1]
+    for a, b in zip(starts, np.r_[starts[1:], C]):
+        ordinal[order[a:b]] = np.arange(b - a)
+    counts = np.bincount(wg, minlength=G)[:G]
+    print("clips per workgroup: min %d p50 %d max %d" % (counts.min(), np.median(counts), counts.max()))
+    for o in (0, 1, 2, 3, 5, 8, 12, 16, 24, 48, 96, 128):
+        m = ordinal == o
+        if m.sum() >= 16:
+            print("  ordinal %3d: n %5d span mean %.2f p50 %.2f p90 %.2f us" % (o, m.sum(), span[m].mean(), np.median(span[m]),
+                                                                        np.percentile(span[m], 90)))
+    print("  span percentiles p50 %.2f p75 %.2f p90 %.2f p99 %.2f max %.2f" % tuple(np.percentile(span, [50, 75, 90, 99, 100])))
