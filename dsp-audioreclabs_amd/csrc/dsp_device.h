@@ -500,6 +500,48 @@ __device__ __forceinline__ void wave_bitonic(K (&a)[NH], int lane)
         }
     }
 }
+// the r-th and (r+1)-th smallest (0-based, wave-uniform r) of the 32-bit keys a[0..NH-1] of all 64
+// lanes, by a ballot radix select from the top bit: per bit one v_bfe + compare per register, the
+// candidate sets and counts in scalar registers -- 2 NH VALU per bit against bitonic's ~7 NH per
+// compare-exchange stage (21 stages for 64 keys, 28 for 128).  Pads must be ~0u and r + 1 < the
+// number of real keys (or r + 1 == it with r1 then read as the r-th's successor, which exists).
+template <int NH>
+__device__ __forceinline__ void wave_select2(const unsigned (&a)[NH], int r, unsigned &k0, unsigned &k1)
+{
+    unsigned long long cand[NH];
+#pragma unroll
+    for (int h = 0; h < NH; h++) cand[h] = ~0ull;
+    unsigned pre = 0;
+    int rr = r;
+#pragma unroll
+    for (int b = 31; b >= 0; b--) {
+        unsigned long long z[NH];
+        int zeros = 0;
+#pragma unroll
+        for (int h = 0; h < NH; h++) {
+            z[h] = cand[h] & ~__ballot(__builtin_amdgcn_ubfe(a[h], b, 1) != 0u);
+            zeros += __popcll(z[h]);
+        }
+        const bool low = rr < zeros;  // wave-uniform
+#pragma unroll
+        for (int h = 0; h < NH; h++) cand[h] = low ? z[h] : cand[h] & ~z[h];
+        rr = low ? rr : rr - zeros;
+        pre = low ? pre : pre | (1u << b);
+    }
+    k0 = pre;
+    // the (r+1)-th: the same key when more than rr + 1 keys equal it, else the smallest key above
+    int eq = 0;
+#pragma unroll
+    for (int h = 0; h < NH; h++) eq += __popcll(cand[h]);
+    if (rr + 1 < eq) {
+        k1 = pre;
+    } else {
+        unsigned m = ~0u;
+#pragma unroll
+        for (int h = 0; h < NH; h++) m = min(m, a[h] > pre ? a[h] : ~0u);
+        k1 = (unsigned)wave_reduce((int)(m ^ 0x80000000u), OpMin()) ^ 0x80000000u;  // unsigned min
+    }
+}
 template <int NH, typename K>
 __device__ __forceinline__ K sorted_at(const K (&a)[NH], int r)  // wave-uniform r
 {

@@ -756,6 +756,13 @@ __device__ __forceinline__ ClipStats clip_stats(const Shared *sh, int n, int L, 
 // p90 order statistics of the VAD energies (:198) by ONE wave, nv <= 128: bitonic sort of the high
 // halves of the order-preserving keys; the rank's element is the one holding that high half, or,
 // when several do, the one of the right rank among them by the full key -> c.sh->pa / pb
+// p90 and the medians by a ballot radix select (wave_select2) instead of bitonic sorts: 70% of
+// the VALU of those phases, but three times the SALU, and the CU's scalar unit is shared by its 24
+// waves: 100k clips 2.64 -> 2.71 ms, 12.5k unchanged (profiles/r05rs_ab_select.txt).  1: both,
+// 2: p90 only, 0: neither
+#ifndef EXTRACT_SELECT_RADIX
+#define EXTRACT_SELECT_RADIX 0
+#endif
 __device__ __forceinline__ void p90_select_wave(const Ctx &c, int nv, int lane)
 {
     const double vi = (double)(nv - 1) * 0.9;
@@ -770,9 +777,16 @@ __device__ __forceinline__ void p90_select_wave(const Ctx &c, int nv, int lane)
     const unsigned long long f1 = lane + 64 < nv ? dkey(c.vE[lane + 64]) : ~0ull;
     const unsigned h0 = (unsigned)(f0 >> 32), h1 = (unsigned)(f1 >> 32);
     unsigned a[2] = {h0, h1};
-    wave_bitonic<2>(a, lane);
+    unsigned ka, kb;  // the high key words at ranks r0 and r1 (EXTRACT_SELECT_RADIX) ...
+    if (EXTRACT_SELECT_RADIX) {  // 1 or 2
+        wave_select2<2>(a, r0, ka, kb);
+    } else {  // ... or read from a bitonic sort of them
+        wave_bitonic<2>(a, lane);
+        ka = sorted_at<2>(a, r0);
+        kb = sorted_at<2>(a, r1);
+    }
     auto full_at = [&](int r) -> double {
-        const unsigned kh = sorted_at<2>(a, r);  // never the pad's ~0u: r < nv
+        const unsigned kh = r == r0 ? ka : kb;  // never the pad's ~0u: r < nv
         const unsigned long long c0 = __ballot(h0 == kh), c1 = __ballot(h1 == kh);
         if (__popcll(c0) + __popcll(c1) == 1)
             return dkey_value(c0 ? lane_read(f0, __ffsll((long long)c0) - 1)
@@ -973,7 +987,17 @@ __device__ __forceinline__ void r5_fast(const Ctx &c, int F, float *featb, int w
         if (job < 3) {  // median by an in-wave bitonic sort
             unsigned a[2] = {in0 ? fkey(x0) : ~0u, in1 ? fkey(x1) : ~0u};
             float v0, v1;
-            if (F <= 64) {
+            if (EXTRACT_SELECT_RADIX == 1) {  // r1 = r0 or r0 + 1 < F
+                unsigned k0, k1;
+                if (F <= 64) {
+                    const unsigned b[1] = {a[0]};
+                    wave_select2<1>(b, r0, k0, k1);
+                } else {
+                    wave_select2<2>(a, r0, k0, k1);
+                }
+                v0 = fkey_value(k0);
+                v1 = fkey_value(r1 == r0 ? k0 : k1);
+            } else if (F <= 64) {
                 unsigned b[1] = {a[0]};
                 wave_bitonic<1>(b, lane);
                 v0 = fkey_value(sorted_at<1>(b, r0));
