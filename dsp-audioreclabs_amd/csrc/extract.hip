@@ -2019,8 +2019,12 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
                                                  (int)(EXTRACT_LDS_LIMIT / lds_launch)));
     const int slots = per_cu * num_cus;
     const int grid = B < slots ? B : slots;
-    // short batches: a finer tail; at most two clips per workgroup: the static split (no claims)
-    p.qchunk = B <= 2 * (int64_t)grid ? 0 : B < 64 * (int64_t)grid ? 2 : 4;
+    // short batches: a finer tail
+    // up to 1.5 clips per workgroup the static split (the second clips start on no claim; 1 000
+    // clips: 0.056 against 0.060 ms per step with 1-clip chunks), up to 2 claimed 1-clip chunks (the
+    // workgroups done first take them; 1 500 clips: 0.075 against 0.081 ms static;
+    // profiles/r05d1_ab_short.txt)
+    p.qchunk = 2 * B <= 3 * (int64_t)grid ? 0 : B <= 2 * (int64_t)grid ? 1 : B < 64 * (int64_t)grid ? 2 : 4;
     static_assert(EXTRACT_OSTAGE >= 4, "qchunk <= EXTRACT_OSTAGE");
     const hipStream_t s = (hipStream_t)stream;
     if (fast) {

@@ -155,3 +155,29 @@ def test_two_streams_concurrent_and_static_split():
     torch.cuda.synchronize()
     for k in ref_a:
         assert torch.equal(out[k], ref_a[k]), k
+
+
+@pytest.mark.gpu
+def test_queue_modes_same_bits():
+    """Every clip-queue mode gives the static split's bits: 1 000 clips (<= 1.5 per workgroup: the
+    static split), 1 400 (1-clip claimed chunks), 4 000 (2-clip chunks), and each against the
+    C ABI's queue_ws = NULL launch of the same clips."""
+    import torch
+    from src import _hip
+    from src.pipeline import FeatureExtractor
+    from src.synth import make_batch
+    fx = FeatureExtractor(L, S, "hamming", True)
+    for B in (1000, 1400, 4000):
+        x = torch.as_tensor(make_batch(B, base_seed=900 + B)).cuda()
+        ref = {k: v.clone() for k, v in fx(x).items()}
+        out = {k: torch.empty_like(v) for k, v in ref.items()}
+        flat = x.reshape(-1)
+        off = torch.arange(B + 1, dtype=torch.int64, device="cuda") * x.shape[1]
+        P = _hip.ptr
+        rc = _hip.lib().dsp_extract_features(P(flat), P(off), B, x.shape[1], L, S, P(fx.window), 1, 0.5, 0.1, 1.5,
+                                             P(out["feat"]), P(out["start_end"]), P(out["n_frames"]),
+                                             P(out["status"]), None, None, 0, None, 0, None, _hip.stream_handle())
+        _hip.check(rc, "dsp_extract_features")
+        torch.cuda.synchronize()
+        for k in ref:
+            assert torch.equal(out[k], ref[k]), (B, k)
