@@ -153,6 +153,26 @@ struct Shared {
 static_assert(sizeof(Shared) <= EXTRACT_SHARED_BYTES, "grow EXTRACT_SHARED_BYTES");
 static_assert((EXTRACT_OSTAGE & (EXTRACT_OSTAGE - 1)) == 0 && EXTRACT_OSTAGE <= 32, "chunk of 2^k <= 32 clips");
 
+// The kernel's parameter block in its kernarg segment (the only explicit argument, offset 0), read
+// again where rarely used fields are needed -- an s_load from the constant cache each time --
+// instead of holding their pointers in SGPRs across the clip loop.  FAST SGPR spills 33 -> 8, but
+// 2.62-2.63 -> 2.67 ms at 100k clips: each s_load's lgkmcnt wait also waits for the wave's LDS
+// operations (profiles/r05kr_ab_kargs.txt).  Off; kept for A/B.
+#ifndef EXTRACT_KARGS_RELOAD
+#define EXTRACT_KARGS_RELOAD 0
+#endif
+__device__ __forceinline__ const ExtractParams &kargs(const ExtractParams &p)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (!EXTRACT_KARGS_RELOAD) return p;
+    const ExtractParams *q = (const ExtractParams *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(q));
+    return *q;
+#else
+    return p;  // (host pass of the device code)
+#endif
+}
+
 struct ClipRef {
     int64_t base;  // 8-aligned first sample index of the clip's vectors
     int lead, n, nvec, nword;
@@ -305,11 +325,12 @@ __device__ __forceinline__ int vad_scan(const ExtractParams &p, const Ctx &c, in
     const double g = (vi >= (double)(nv - 1)) ? vi + 1.0 : vi - floor(vi);
     const double p90 = np_lerp(sh->pa, sh->pb, g);
     double t1, t2, tz;
+    const ExtractParams &q = kargs(p);
     {
 #pragma clang fp contract(off)
-        t1 = p90 * p.hi;                        // :202
-        t2 = noise_e + (p90 - noise_e) * p.lo;  // :217
-        tz = noise_z * p.zr;                    // :247
+        t1 = p90 * q.hi;                        // :202
+        t2 = noise_e + (p90 - noise_e) * q.lo;  // :217
+        tz = noise_z * q.zr;                    // :247
     }
     STAMP(c.stamp_clip, 10);
     auto near = [&](double e, double t) {
@@ -1636,10 +1657,11 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
             st = sh->n1 * S;              // :272
             en = min(sh->n6 * S + L, n);  // :273
         }
-        if (p.vad_energy)
-            for (int f = opaque_tid(); f < nv && f < p.ld_vad; f += NT) {
-                p.vad_energy[(size_t)i * p.ld_vad + f] = c.vE[f];
-                p.vad_zcr[(size_t)i * p.ld_vad + f] = c.vZ[f];
+        const ExtractParams &q = kargs(p);
+        if (q.vad_energy)
+            for (int f = opaque_tid(); f < nv && f < q.ld_vad; f += NT) {
+                q.vad_energy[(size_t)i * q.ld_vad + f] = c.vE[f];
+                q.vad_zcr[(size_t)i * q.ld_vad + f] = c.vZ[f];
             }
     }
     STAMP(i, 4);
@@ -1667,9 +1689,10 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     }
     STAMP(i, 9);
     MARK(tail);
-    if (p.seq)
-        for (int g = tid; g < F && g < p.ld_seq; g += NT) {
-            float *o = p.seq + ((size_t)i * p.ld_seq + g) * 3;
+    const ExtractParams &qs = kargs(p);
+    if (qs.seq)
+        for (int g = tid; g < F && g < qs.ld_seq; g += NT) {
+            float *o = qs.seq + ((size_t)i * qs.ld_seq + g) * 3;
             o[0] = c.fE[g];
             o[1] = c.fM[g];
             o[2] = (float)c.fZ[g];
@@ -1690,13 +1713,14 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
 
 __device__ __forceinline__ void write_bad_clip(const ExtractParams &p, int i, int tid)
 {
-    if (tid < 15) p.feat[(size_t)i * 15 + tid] = __builtin_nanf("");
+    const ExtractParams &q = kargs(p);
+    if (tid < 15) q.feat[(size_t)i * 15 + tid] = __builtin_nanf("");
     if (tid == 0) {
-        const int64_t nn = p.offsets[i + 1] - p.offsets[i];
-        p.status[i] = nn <= 0 ? DSP_CLIP_EMPTY : DSP_CLIP_TOO_LONG;
-        p.start_end[2 * i] = 0;
-        p.start_end[2 * i + 1] = 0;
-        p.n_frames[i] = 0;
+        const int64_t nn = q.offsets[i + 1] - q.offsets[i];
+        q.status[i] = nn <= 0 ? DSP_CLIP_EMPTY : DSP_CLIP_TOO_LONG;
+        q.start_end[2 * i] = 0;
+        q.start_end[2 * i + 1] = 0;
+        q.n_frames[i] = 0;
     }
 }
 
@@ -1787,16 +1811,17 @@ __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &
 // sectors once L2 has evicted the lines between neighbouring clips' writes
 __device__ __forceinline__ void flush_outputs(const ExtractParams &p, const Ctx &c, int done, int tid)
 {
+    const ExtractParams &q = kargs(p);
     constexpr int CH = EXTRACT_OSTAGE;
     const int cb = done & ~(CH - 1);
     // nothing staged for this chunk (its clips were deferred or bad: written directly) -> 0
     const unsigned m = c.sh->schunk == cb / CH ? c.sh->smask : 0u;
     for (int t = tid; t < 15 * CH; t += NT)
-        if ((m >> (t / 15)) & 1) p.feat[(size_t)cb * 15 + t] = c.ofeat[t];
-    if (tid < 2 * CH && ((m >> (tid >> 1)) & 1)) p.start_end[2 * (size_t)cb + tid] = c.ose[tid];
+        if ((m >> (t / 15)) & 1) q.feat[(size_t)cb * 15 + t] = c.ofeat[t];
+    if (tid < 2 * CH && ((m >> (tid >> 1)) & 1)) q.start_end[2 * (size_t)cb + tid] = c.ose[tid];
     if (tid < CH && ((m >> tid) & 1)) {
-        p.n_frames[cb + tid] = c.onf[tid];
-        p.status[cb + tid] = c.ost[tid];
+        q.n_frames[cb + tid] = c.onf[tid];
+        q.status[cb + tid] = c.ost[tid];
     }
 }
 
@@ -1878,8 +1903,8 @@ void extract_kernel(ExtractParams p)
                 if (!done && tid == 0) sh->next = queue_end(Q, sh, cl);  // a deferred clip returns before R4
             }
             if (!done && tid == 0) {
-                p.status[i] = DSP_CLIP_UNCERTIFIED;
-                if (p.queue) __hip_atomic_fetch_add(qword(p.queue, 9), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                kargs(p).status[i] = DSP_CLIP_UNCERTIFIED;
+                if (kargs(p).queue) __hip_atomic_fetch_add(qword(kargs(p).queue, 9), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             inflight = (FAST ? EXTRACT_FAST_PREFETCH > 0 : EXTRACT_PREFETCH) && done;
             pre = -1;
