@@ -219,7 +219,7 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
-    from src.distributed import gather_packed, shard_range
+    from src.distributed import gather_rows, shard_range
     from src.pipeline import FeatureExtractor
     from src.synth import make_batch_device
 
@@ -256,7 +256,11 @@ def main():
     graph = None
     if not args.no_graph:
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=torch.cuda.Stream(dev)):
+        cs = torch.cuda.Stream(dev)
+        with torch.cuda.stream(cs):  # the capture stream's own clip-queue scratch, outside the graph
+            fx(pool[0])
+        cs.synchronize()
+        with torch.cuda.graph(graph, stream=cs):
             for i in range(K):
                 fx(pool[i % P])
         graph.replay()
@@ -275,6 +279,16 @@ def main():
         dist.barrier()
     elapsed_x = time.perf_counter() - t0  # extraction only
     my_frames = float(sum(frames[i % P] for i in range(K)))
+    # the timed steps checked: the last replayed step's outputs (still in the extractor's buffers)
+    # against one eager launch of the same batch into fresh buffers, bit for bit
+    timed_ok = None
+    if graph is not None:
+        got = fx._outputs(C, N)["rows"].clone()
+        fresh = FeatureExtractor(L, S, args.window, vad, device=dev)
+        ref = fresh(pool[(K - 1) % P])["rows"]
+        torch.cuda.synchronize(dev)
+        timed_ok = bool(torch.equal(got, ref))
+        del fresh, ref, got
     del graph
 
     # N > 1: configs[3] as BASELINE defines it -- every step is the rank's extraction followed by
@@ -283,8 +297,7 @@ def main():
     elapsed_g, ag = None, None
     if world > 1:
         def step(b):
-            out = fx(b)
-            return gather_packed({k: out[k] for k in ("feat", "start_end", "n_frames", "status")}, args.clips)
+            return gather_rows(fx(b)["rows"], args.clips)
         step(pool[0])
         torch.cuda.synchronize(dev)
         dist.barrier()
@@ -296,19 +309,19 @@ def main():
         dist.barrier()
         elapsed_g = time.perf_counter() - t0
         # the all-gather alone (median of 5), for the record
-        out = fx(pool[0])
-        res = {k: out[k] for k in ("feat", "start_end", "n_frames", "status")}
+        rows = fx(pool[0])["rows"]
         torch.cuda.synchronize(dev)
         ts = []
         for _ in range(5):
             dist.barrier()
             g0 = time.perf_counter()
-            gather_packed(res, args.clips)
+            gather_rows(rows, args.clips)
             torch.cuda.synchronize(dev)
             ts.append(time.perf_counter() - g0)
         ag = {"ms": round(float(np.median(ts)) * 1e3, 4), "bytes": args.clips * OUT_BYTES_PER_CLIP,
               "collectives": 1, "backend": backend_name,
-              "what": "feat/start_end/n_frames/status of all clips, packed, one %s all_gather" % backend_name}
+              "what": "every clip's packed 76-B result row (feat, start/end, n_frames, status) as written by "
+                      "the kernel, one %s all_gather_into_tensor, no pack/unpack kernels" % backend_name}
     if world > 1:
         t = torch.tensor([elapsed_x, elapsed_g, my_frames, kern_ms], dtype=torch.float64, device=dev)
         tmax = t.clone()
@@ -316,18 +329,27 @@ def main():
         tsum = t.clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         elapsed_x, elapsed_g, total_frames, kern_ms = tmax[0].item(), tmax[1].item(), tsum[2].item(), tmax[3].item()
+        if timed_ok is not None:  # every rank's last timed step
+            ok = torch.tensor([1 if timed_ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            timed_ok = bool(ok.item())
     else:
         total_frames = my_frames
 
     sweep = window_sweep(args, fx, pool[0], dev, world, rank) if args.sweep_clips > 0 else None
     cfg0 = configs0_leg(args, pool[0], dev, world) if args.cfg0 else None
     cfg1 = configs1_leg(args, fx, pool[0], dev, world) if args.small_clips > 0 else None
-    knn = knn_leg(args, dev, world, rank) if args.knn_ref > 0 else None
+    knn = knn_leg(args, fx, pool[0], dev, world, rank) if args.knn_ref > 0 else None
 
     result = None
     if rank == 0:
         result = assemble_result(args, world, ranks_seen, rehearsal, backend_name, C, total_frames, elapsed_x,
                                  elapsed_g, kern_ms)
+        result["timed_outputs_equal"] = timed_ok
+        if timed_ok is not None:
+            result["timed_outputs_check"] = ("the last replayed step's packed rows (feat, start/end, n_frames, "
+                                             "status of all %d clips per rank) against one eager launch of the same "
+                                             "batch into fresh buffers, bitwise" % C)
         if ag is not None:
             result["allgather"] = ag
         if cfg0 is not None:
@@ -340,6 +362,8 @@ def main():
             result["knn"] = knn
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(fx, pool[0], L, S, args.window, vad, args.cpu_seconds)
+            result["cpu_baseline_reference_semantics"] = cpu_baseline_reference_semantics(
+                pool[0], L, S, args.window, vad, args.cpu_seconds * 0.75)
             if cfg0 is not None:
                 fx0 = FeatureExtractor(1024, 512, "hamming", True, device=dev)
                 cfg0["cpu_baseline"] = cpu_baseline(fx0, pool[0], 1024, 512, "hamming", True, args.cpu_seconds / 2)
@@ -429,24 +453,33 @@ def configs1_leg(args, fx, batch, dev, world):
             "frames_per_s_kernel": round(fr / (ms * 1e-3), 1)}
 
 
-def knn_leg(args, dev, world, rank):
+def knn_leg(args, fx, batch, dev, world, rank):
     """BASELINE configs[4] beside the headline metric: exact k-NN (KNeighborsClassifier
-    semantics) of every one of --knn-ref synthetic z-scored 15-d vectors against all of them
-    (self excluded), queries sharded over the ranks, results gathered (one RCCL all-gather).
-    Not part of ``value``; reported as its own object with its fp32 roofline: 45 algorithmic flop per
-    pair (15 sub + 15 mul + 15 add) against 157.3 TF/s, the fp32 peak of both the matrix cores
-    (v_mfma_f32_16x16x4_f32, the screen's distances) and the VALU."""
+    semantics) on the EXTRACTED feature vectors of the north-star batch, as the reference chains
+    them (experiments/run_experiments.py:262-280, src/models.py:33-35): each rank's extraction of
+    its shard -> one gather of the packed result rows (every rank holds every clip's 15-d vector)
+    -> normalize_features on the device (dsp_zscore_fit / dsp_zscore_apply, fp64) -> the first
+    --knn-ref vectors each queried against all of them (self excluded, k = --knn-k), queries
+    sharded over the ranks, (idx, dist, pred) gathered in one collective.  Labels are clip index
+    mod 10 (the synthetic batch has no classes; they only feed the vote).  Timed: the sharded
+    search + its gather (median of 3).  Not part of ``value``; reported with its fp32 roofline:
+    45 algorithmic flop per pair (15 sub + 15 mul + 15 add) against 157.3 TF/s, the fp32 peak of
+    both the matrix cores (v_mfma_f32_16x16x4_f32, the screen's distances) and the VALU."""
     import torch
     import torch.distributed as dist
-    from src.distributed import knn_sharded
-    from src.pipeline import knn_classify
-    rng = np.random.default_rng(0)  # same reference set on every rank
-    n, dim = args.knn_ref, 15
-    centres = rng.standard_normal((10, dim)) * 1.5
-    y = rng.integers(0, 10, n).astype(np.int32)
-    X = centres[y] + rng.standard_normal((n, dim))
-    X = (X - X.mean(0)) / X.std(0)
-    Xd, yd = torch.as_tensor(X, device=dev), torch.as_tensor(y, device=dev)
+    from src.distributed import gather_rows, knn_sharded, result_views
+    from src.pipeline import knn_classify, zscore_apply, zscore_fit
+    res = result_views(gather_rows(fx(batch)["rows"], args.clips))
+    assert not (res["status"] & 0xFF).any().item()
+    n = min(args.knn_ref, args.clips)
+    feat = res["feat"][:n].to(torch.float64)
+    torch.cuda.synchronize(dev)
+    z0 = time.perf_counter()
+    mu, sd = zscore_fit(feat)
+    Xd = zscore_apply(feat, mu, sd)
+    torch.cuda.synchronize(dev)
+    zs_ms = (time.perf_counter() - z0) * 1e3
+    yd = (torch.arange(n, device=dev) % 10).to(torch.int32)
     knn_sharded(knn_classify, Xd, yd, Xd, args.knn_k, self_query=True)  # warm-up
     torch.cuda.synchronize(dev)
     ts = []
@@ -461,29 +494,44 @@ def knn_leg(args, dev, world, rank):
             dist.barrier()
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
+    # untimed: how many queries the fp32 screen could not certify (exhaustive fp64 fallback)
+    from src.distributed import shard_range
+    lo, hi = shard_range(n, rank, world)
+    st = {}
+    knn_classify(Xd, yd, Xd[lo:hi], args.knn_k, self_offset=lo, n_classes=10, stats=st)
+    fb = torch.tensor([float(st.get("fallbacks", 0))], dtype=torch.float64, device=dev)
     if world > 1:
         tt = torch.tensor([t], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = tt.item()
+        dist.all_reduce(fb)
+    X = Xd.cpu().numpy()
+    y = yd.cpu().numpy()
     pairs = float(n) * n
     tf = pairs * 45 / t / 1e12
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0:
         # the C oracle (sklearn semantics, fp64) on a bounded sample of the same queries, timed on
         # the host cores; the answers of the last timed run for those queries must equal it bit
         # for bit
         idx, dist_, pred = last
         cpu = knn_cpu_baseline(X, y, args.knn_k, idx, dist_, pred)
-    res = {"metric": "k-NN pairs/s (15-d, exact, k=%d, self-query, gathered)" % args.knn_k,
+    out = {"metric": "k-NN pairs/s (15-d, exact, k=%d, self-query, gathered)" % args.knn_k,
             "value": round(pairs / t, 1), "unit": "pairs/s", "ms": round(t * 1e3, 4),
             "ref": n, "queries": n, "queries_per_rank": -(-n // world),
             "roofline": {"bound": "mfma-f32", "achieved": round(tf, 2), "peak": 157.3 * world, "unit": "TFLOP/s",
                          "frac": round(tf / (157.3 * world), 4), "flop_per_pair": 45,
                          "note": "whole-job wall time incl. conversion, merge and the result all-gather"},
-            "data": "synthetic z-scored 15-d vectors around 10 class centres"}
+            "data": "extracted features: the z-scored 15-d statistics the fused kernel produced for the first %d "
+                    "clips of the north-star batch (gathered over %d rank(s), normalize_features on the device "
+                    "%.2f ms); labels clip index mod 10" % (n, world, zs_ms),
+            "fallbacks": int(fb.item()),
+            "fallbacks_note": "queries the fp32 screen could not certify, answered by the exhaustive fp64 scan"}
     if cpu is not None:
-        res["cpu_baseline"] = cpu
-    return res
+        out["parity_on_sample"] = cpu.pop("parity_on_sample")
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu
+    return out
 
 
 def knn_cpu_baseline(X, y, k, idx, dist, pred, nq=1000):
@@ -566,6 +614,59 @@ def cpu_baseline(fx, batch, L, S, window, vad, budget_s):
             "parity_on_sample": {"clips": C, "start_end_exact": se_ok, "n_frames_exact": nf_ok,
                                  "feat_max_rel_err": float(np.nanmax(rel)),
                                  "feat_cells_over_1e-5_rel": int(np.nansum(rel > 1e-5))}}
+
+
+def cpu_baseline_reference_semantics(batch, L, S, window, vad, budget_s, n_sample=1000):
+    """SURVEY.md §8d's baseline as the reference runs it: its own numpy algorithm, one clip at a
+    time with a Python loop over frames (oracle/np_reference.py, bit-exact against the reference's
+    golden vectors), over a process pool of every usable host core, on a bounded sample of the
+    benchmark's clips.  Its outputs on the sample are checked against the C oracle (start/end,
+    frame counts and all 15 features bit for bit)."""
+    import multiprocessing as mp
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import np_reference
+    import oracle
+    from src.pipeline import create_window
+    w = create_window(window, L)
+    host = batch[:n_sample].cpu().numpy()
+    C, N = host.shape
+    threads, visible, quota = host_cores()
+    nv = (N - L) // S + 1 if (vad and N >= L) else 0
+    per = -(-C // (4 * threads))  # ~4 tasks per worker
+    tasks = [(host[a:a + per], L, S, w, vad) for a in range(0, C, per)]
+    # spawned workers (fresh interpreters): nothing GPU-side is inherited by a fork
+    with mp.get_context("spawn").Pool(threads) as pool:
+        pool.map(np_reference.process_many, [(host[:2], L, S, w, vad)] * threads)  # start-up, imports
+        passes, t_total, frames = 0, 0.0, 0
+        first = None
+        while passes == 0 or (t_total < budget_s and passes < 50):
+            t0 = time.perf_counter()
+            res = pool.map(np_reference.process_many, tasks)
+            t_total += time.perf_counter() - t0
+            passes += 1
+            nf = np.concatenate([r[3] for r in res])
+            frames += int(nf.sum()) + nv * C
+            if first is None:
+                first = res
+    st = np.concatenate([r[0] for r in first])
+    feat = np.concatenate([r[1] for r in first])
+    se = np.concatenate([r[2] for r in first])
+    nf = np.concatenate([r[3] for r in first])
+    flat = np.ascontiguousarray(host.reshape(-1))
+    ref = oracle.process_batch(flat, np.arange(C + 1, dtype=np.int64) * N, L, S, w, do_vad=vad, nthreads=threads)
+    ok = ref["status"] == 0
+    t1 = time.perf_counter()
+    np_reference.process_many((host[:20], L, S, w, vad))  # one process, for the per-core rate
+    one = (nv * 20 + int(nf[:20].sum())) / (time.perf_counter() - t1)
+    return {"value": round(frames / t_total, 1), "unit": "frames/s", "cores": threads, "kind": "reference-semantics",
+            "sample": "%d passes over %d of the benchmark's clips (%.1f s): the reference's numpy algorithm as it "
+                      "runs (per-clip, per-frame Python loop; oracle/np_reference.py, bit-exact against the "
+                      "reference's golden vectors) on a spawn pool of %d processes (all usable cores); 1 process: "
+                      "%.4g frames/s" % (passes, C, t_total, threads, one),
+            "parity_vs_c_oracle": {"clips": C, "status_equal": bool(np.array_equal(st, ref["status"])),
+                                   "start_end_equal": bool(np.array_equal(se[ok], ref["start_end"][ok])),
+                                   "n_frames_equal": bool(np.array_equal(nf[ok], ref["n_frames"][ok])),
+                                   "feat_bit_exact": bool(np.array_equal(feat[ok], ref["feat"][ok]))}}
 
 
 if __name__ == "__main__":

@@ -306,6 +306,14 @@ __device__ __forceinline__ int sq2(short2v d)
     return r;
 }
 
+// acc + k0^2 + k1^2 in one v_dot2_i32_i16 (32-bit, wrapping)
+__device__ __forceinline__ int sq2acc(short2v d, int acc)
+{
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %1, %2" : "=v"(r) : "v"(d), "v"(acc));
+    return r;
+}
+
 __device__ __forceinline__ short2v half_pair(const short8 &x, int i)
 {
     switch (i) {

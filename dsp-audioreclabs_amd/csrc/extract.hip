@@ -1,15 +1,16 @@
 // extract.hip -- fused per-clip feature extraction for gfx950 (CDNA4).
 //
-// Persistent workgroups (512 threads, two per CU) walk the batch, one clip at a time.  The clip is
-// read from HBM once, straight into registers (each thread holds EXTRACT_RREG 32-sample words):
+// Persistent workgroups (512 threads, three per CU on the compile-time layout, two on the generic
+// one) walk the batch, one clip at a time.  The clip is read from HBM once, straight into
+// registers (each thread holds EXTRACT_RREG 32-sample words):
 //   R1  registers: integer sum / min / max + exact per-word moments (sum k, sum k^2) -> LDS
 //   R2  registers: positive-sample bits per word -> LDS (the ZCR of any range is a popcount)
-//   R3  endpoint detection from the per-word summaries (+ the two partial words of each frame,
-//       re-read from L2), p90 by a one-wave bitonic sort, double-threshold scan
+//   R3  endpoint detection from the per-word summaries (+ the two partial words of each frame),
+//       p90 by a one-wave bitonic sort, double-threshold scan
 //   R4  windowed frames of the crop (clip-relative vectors re-read from L2, window from LDS)
 //   R5  15-d statistics
-// LDS holds only summaries, the window table and the per-frame arrays (~54 KB in the compile-time
-// layout), so a second workgroup on the same CU computes while this one waits for HBM.
+// LDS holds only summaries, the window table and the per-frame arrays (48 992 B in the
+// compile-time layout), so the other workgroups on the same CU compute while one waits for HBM.
 // Algorithmic traffic: 2 B/sample in + 76 B/clip out.
 //
 // Reference functions restated (Hypersonic-cpu/DSP-AudioRecLabs):
@@ -39,18 +40,9 @@
 #include "extract_layout.h"
 #include "dsp_device.h"
 
-#ifndef DSP_ABL  // diagnostic ablation builds only (tools/ablate_build.sh; outputs are wrong): skip
-#define DSP_ABL 0 // 1 = R4 frames, 2 = R5 jobs, 4 = R2 sign bits, 8 = VAD pass-A partial moments
-#endif
-
-// 1: a clip's words are loaded while the previous clip's R5 runs (its registers live across R5);
-// 0: at the clip's start (the co-resident workgroups cover the wait)
-#ifndef EXTRACT_STATS_W0
-#define EXTRACT_STATS_W0 1
-#endif
-#ifndef EXTRACT_PREFETCH
-#define EXTRACT_PREFETCH 1
-#endif
+#ifndef DSP_ABL  // the phase-ablation instrument (tools/ablate_build.sh, diagnostic builds only;
+#define DSP_ABL 0 // outputs are wrong): skip 1 = R4 frames, 2 = R5 jobs, 4 = R2 sign bits,
+#endif            // 8 = VAD pass-A partial moments -- the per-phase VALU budget of DESIGN.md §8
 
 namespace dsp {
 
@@ -109,6 +101,7 @@ struct ExtractParams {
     double hi, lo, zr;
     float *feat;
     int32_t *start_end, *n_frames, *status;
+    int ostride;  // 0: feat [B,15], start_end [B,2], n_frames / status [B]; > 0: row b of each at b * ostride
     double *vad_energy;
     int32_t *vad_zcr;
     int ld_vad;
@@ -118,9 +111,15 @@ struct ExtractParams {
     unsigned *queue;             // caller's clip-queue scratch (NULL: static split), zero at launch;
                                  // the last workgroup out zeroes it again
     int qchunk;                  // clips per queue chunk (host: 4, 2 for short batches, 0: static split)
-    ExtractCarve cv;             // LDS layout, computed on the host (kernel arguments can be
-                                 // re-read instead of being held in registers)
+    ExtractCarve cv;             // LDS layout, computed on the host
 };
+
+// the clip's output rows: per-array [B,15] / [B,2] / [B] / [B], or rows of p.ostride 4-byte words
+// (ABI 6: one packed [B, DSP_OUT_ROW_WORDS] buffer with the four arrays as column ranges)
+__device__ __forceinline__ float *out_feat(const ExtractParams &p, int i) { return p.feat + (size_t)i * (p.ostride ? p.ostride : 15); }
+__device__ __forceinline__ int32_t *out_se(const ExtractParams &p, int i) { return p.start_end + (size_t)i * (p.ostride ? p.ostride : 2); }
+__device__ __forceinline__ int32_t *out_nf(const ExtractParams &p, int i) { return p.n_frames + (size_t)i * (p.ostride ? p.ostride : 1); }
+__device__ __forceinline__ int32_t *out_st(const ExtractParams &p, int i) { return p.status + (size_t)i * (p.ostride ? p.ostride : 1); }
 
 static_assert(__is_standard_layout(ExtractParams) && __is_trivially_copyable(ExtractParams),
               "ExtractParams is a plain kernel argument block");
@@ -130,13 +129,13 @@ static_assert(sizeof(ExtractParams) <= 1024, "kernel argument block");
 struct ClipStatsRaw {
     double mq, Mp, invM2;
     float invMf;
-    int tpos, t0, nv;
+    int tpos, t0, nv, kneg;
 };
 struct Shared {
     long long red_k[NWAVE];
     int red_a[NWAVE], red_b[NWAVE];
     double pa, pb;            // the two order statistics of the VAD energies around p90
-    ClipStatsRaw cs;          // EXTRACT_STATS_W0: the clip statistics, computed by wave 0
+    ClipStatsRaw cs;          // the clip statistics, computed by wave 0
     double noise_e, noise_z;  // VAD noise estimates (:189-195, :239-245)
     double oslo[3], oshi[3];  // order statistics (F-1)/2 and F/2 of E, M, ZCR (medians)
     int n3, n1, n6, exact, j0, j1, next;
@@ -152,26 +151,6 @@ struct Shared {
 };
 static_assert(sizeof(Shared) <= EXTRACT_SHARED_BYTES, "grow EXTRACT_SHARED_BYTES");
 static_assert((EXTRACT_OSTAGE & (EXTRACT_OSTAGE - 1)) == 0 && EXTRACT_OSTAGE <= 32, "chunk of 2^k <= 32 clips");
-
-// The kernel's parameter block in its kernarg segment (the only explicit argument, offset 0), read
-// again where rarely used fields are needed -- an s_load from the constant cache each time --
-// instead of holding their pointers in SGPRs across the clip loop.  FAST SGPR spills 33 -> 8, but
-// 2.62-2.63 -> 2.67 ms at 100k clips: each s_load's lgkmcnt wait also waits for the wave's LDS
-// operations (profiles/r05kr_ab_kargs.txt).  Off; kept for A/B.
-#ifndef EXTRACT_KARGS_RELOAD
-#define EXTRACT_KARGS_RELOAD 0
-#endif
-__device__ __forceinline__ const ExtractParams &kargs(const ExtractParams &p)
-{
-#if defined(__HIP_DEVICE_COMPILE__)
-    if (!EXTRACT_KARGS_RELOAD) return p;
-    const ExtractParams *q = (const ExtractParams *)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(q));
-    return *q;
-#else
-    return p;  // (host pass of the device code)
-#endif
-}
 
 struct ClipRef {
     int64_t base;  // 8-aligned first sample index of the clip's vectors
@@ -217,9 +196,8 @@ struct Ctx {
     int *rank;  // rank scratch: nvcap or 3 * fcap ints
     int *pS1;   // partial-word moments at the two ends of each VAD frame (2 * nvcap)
     unsigned long long *pS2;
-    float *ofeat;    // staged outputs of the clips of one chunk, slot = clip mod EXTRACT_OSTAGE:
-    int32_t *ose;    // feat [slot][15], start/end [slot][2], n_frames [slot], status [slot]
-    int32_t *onf, *ost;
+    int32_t *orow;   // staged output rows of the clips of one chunk, slot = clip mod EXTRACT_OSTAGE:
+                     // [slot][19] = feat[15] (f32 bits), start, end, n_frames, status
     int64_t total;
     int stamp_clip;  // clip index for the diagnostic stamps
 };
@@ -325,7 +303,7 @@ __device__ __forceinline__ int vad_scan(const ExtractParams &p, const Ctx &c, in
     const double g = (vi >= (double)(nv - 1)) ? vi + 1.0 : vi - floor(vi);
     const double p90 = np_lerp(sh->pa, sh->pb, g);
     double t1, t2, tz;
-    const ExtractParams &q = kargs(p);
+    const ExtractParams &q = p;
     {
 #pragma clang fp contract(off)
         t1 = p90 * q.hi;                        // :202
@@ -566,6 +544,12 @@ __device__ __forceinline__ double uni(double v)
     return __builtin_bit_cast(double, (long long)(((unsigned long long)hi << 32) | lo));
 }
 
+__device__ __forceinline__ uint64_t uni_u64(uint64_t v)
+{
+    const unsigned lo = __builtin_amdgcn_readfirstlane((int)v), hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // R1 of one 32-sample buffer word w of a clip (lead, n, nword): exact moments (sum k, sum k^2) to
 // wS1[w] / wS2[w]; the thread's running sum K, min and max (packed int16 min / max for the
 // interior words, whose 32 samples are all the clip's)
@@ -628,6 +612,11 @@ __device__ __forceinline__ void r1_word(const short8 *q, int w, int nword, int l
 // and the clip's two edge words -- whose samples outside the clip must not count -- by one wave,
 // a sample per lane re-read from L2 (r1_edges): on the owning lanes the per-sample branches of
 // r1_word's edge loop cost their waves ~300 instructions before the R1 barrier.
+// Sum k^2 of two sample pairs in one 32-bit v_dot2 chain (sq2acc(d1, sq2(d0))), added to the
+// 64-bit word sum once per two pairs: the four squares sum to at most 2^32, and reach it only when
+// all four samples are -32768 -- the chain then wraps to 0.  A clip holding a -32768 sample
+// (ClipStats::kneg, known after the R1 reduction) has its interior word sums redone pair by pair
+// (r1_redo_s2) before anything reads them.
 __device__ __forceinline__ void r1_interior(const short8 *q, int w, R1Acc &a, int *wS1, unsigned long long *wS2)
 {
     int s1 = 0;
@@ -636,16 +625,28 @@ __device__ __forceinline__ void r1_interior(const short8 *q, int w, R1Acc &a, in
 #pragma unroll
     for (int k = 0; k < 4; k++)
 #pragma unroll
-        for (int h = 0; h < 4; h++) {
-            const short2v d = half_pair(q[k], h);
-            a.pmin = __builtin_elementwise_min(a.pmin, d);
-            a.pmax = __builtin_elementwise_max(a.pmax, d);
-            s1 = __builtin_amdgcn_sdot2(d, ones, s1, false);
-            s2 += (unsigned)sq2(d);  // <= 2^31: unsigned
+        for (int h = 0; h < 4; h += 2) {
+            const short2v d0 = half_pair(q[k], h), d1 = half_pair(q[k], h + 1);
+            a.pmin = __builtin_elementwise_min(a.pmin, d0);
+            a.pmax = __builtin_elementwise_max(a.pmax, d0);
+            a.pmin = __builtin_elementwise_min(a.pmin, d1);
+            a.pmax = __builtin_elementwise_max(a.pmax, d1);
+            s1 = __builtin_amdgcn_sdot2(d0, ones, s1, false);
+            s1 = __builtin_amdgcn_sdot2(d1, ones, s1, false);
+            s2 += (unsigned)sq2acc(d1, sq2(d0));  // < 2^32 unless all four are -32768
         }
     wS1[w] = s1;
     wS2[w] = s2;
     a.K += s1;
+}
+__device__ __forceinline__ void r1_redo_s2(const short8 *q, int w, unsigned long long *wS2)
+{
+    unsigned long long s2 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int h = 0; h < 4; h++) s2 += (unsigned)sq2(half_pair(q[k], h));  // <= 2^31: unsigned
+    wS2[w] = s2;
 }
 // lane l: sample l & 31 of the first word (l < 32) or of the last (l >= 32, clips of two words or
 // more); issued at R1's start, consumed (r1_edges) after the interior words
@@ -692,49 +693,31 @@ __device__ __forceinline__ void r1_reduce(const R1Acc &a, Shared *sh, int wid, i
     }
 }
 // R2 of one buffer word: bit b set <=> buffer sample 32w + b is the clip's and k >= tpos (positive
-// after preprocess).  Packed saturating k - tpos per sample pair, the sign bytes gathered by
-// v_perm, their top bits by a multiply (k < tpos), inverted.
-__device__ __forceinline__ uint32_t pos_byte(const short8 &val, short2v tt, bool tbig)
+// after preprocess).  Per 16-B vector (8 samples): each pair's (k - tpos) saturated (v_pk_sub_i16),
+// the four samples of two pairs gathered by ONE v_perm as 0xFF / 0x00 bytes (selectors 8-11
+// replicate the sign bit of bytes 1, 3, 5, 7), and the two gathered dwords weighted (1, 2, 4, 8)
+// and (16, 32, 64, 128) by v_dot4_u32_u8: 255 x the vector's byte of negative samples (+ acc).
+// The word's four values X_k combine as Z = sum 2^(8k) X_k = 255 x NEG (mod 2^32), and with 255
+// added to X_0, Z x 0x01010101 = -(NEG + 1) = ~NEG, the positive bits (255 x 0x01010101 = 2^32 - 1).
+// 35 VALU + one multiply per word against 52 for round 5's per-pair v_pk_lshrrev + v_dot2_u32_u16
+// gather (and round 4's v_perm + quarter-rate multiply per byte).
+__device__ __forceinline__ uint32_t neg_byte255(const short8 &val, short2v tt, uint32_t acc)
 {
-    if (tbig) return 0u;  // tpos > 32767: no int16 sample can be positive
-    const unsigned a0 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 0), tt));
-    const unsigned a1 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 1), tt));
-    const unsigned a2 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 2), tt));
-    const unsigned a3 = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, 3), tt));
-    const unsigned x01 = __builtin_amdgcn_perm(a1, a0, 0x07050301u) & 0x80808080u;
-    const unsigned x23 = __builtin_amdgcn_perm(a3, a2, 0x07050301u) & 0x80808080u;
-    return ~(((x01 * 0x00204081u) >> 28) | (((x23 * 0x00204081u) >> 28) << 4)) & 0xFFu;
-}
-// the same byte without 32-bit multiplies (quarter rate): each pair's (k - tpos) saturated, its
-// sign bits shifted to bit 0 of each half (v_pk_lshrrev_b16), the four pairs weighted (1, 2), (4, 8),
-// (16, 32), (64, 128) and summed by v_dot2_u32_u16 -- the byte of negative samples, inverted
-#ifndef EXTRACT_R2_DOT
-#define EXTRACT_R2_DOT 1
-#endif
-typedef unsigned short ushort2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t neg_byte_dot(const short8 &val, short2v tt)
-{
-    uint32_t b = 0;
+    unsigned a[4];
 #pragma unroll
-    for (int h = 0; h < 4; h++) {
-        const ushort2v sb = __builtin_bit_cast(ushort2v, __builtin_elementwise_sub_sat(half_pair(val, h), tt)) >> 15;
-        const ushort2v wgt = {(unsigned short)(1u << (2 * h)), (unsigned short)(2u << (2 * h))};
-        b = __builtin_amdgcn_udot2(sb, wgt, b, false);
-    }
-    return b;
+    for (int h = 0; h < 4; h++) a[h] = __builtin_bit_cast(unsigned, __builtin_elementwise_sub_sat(half_pair(val, h), tt));
+    const unsigned s03 = __builtin_amdgcn_perm(a[1], a[0], 0x0B0A0908u);  // samples 0-3: 0xFF where k < tpos
+    const unsigned s47 = __builtin_amdgcn_perm(a[3], a[2], 0x0B0A0908u);  // samples 4-7
+    return __builtin_amdgcn_udot4(s47, 0x80402010u, __builtin_amdgcn_udot4(s03, 0x08040201u, acc, false), false);
 }
 __device__ __forceinline__ uint32_t pos_word(const short8 *q, int w, int nword, int lead, int n, int tpos)
 {
     const bool tbig = tpos > 32767;
     const short2v tt = {(short)(tbig ? 32767 : tpos), (short)(tbig ? 32767 : tpos)};
-    uint32_t P;
-    if (EXTRACT_R2_DOT)
-        P = tbig ? 0u
-                 : ~(neg_byte_dot(q[0], tt) | (neg_byte_dot(q[1], tt) << 8) | (neg_byte_dot(q[2], tt) << 16) |
-                     (neg_byte_dot(q[3], tt) << 24));
-    else
-        P = pos_byte(q[0], tt, tbig) | (pos_byte(q[1], tt, tbig) << 8) | (pos_byte(q[2], tt, tbig) << 16) |
-            (pos_byte(q[3], tt, tbig) << 24);
+    const uint32_t x0 = neg_byte255(q[0], tt, 255u), x1 = neg_byte255(q[1], tt, 0u), x2 = neg_byte255(q[2], tt, 0u),
+                   x3 = neg_byte255(q[3], tt, 0u);
+    uint32_t P = tbig ? 0u : ((((x3 << 8) + x2) << 8) + x1 << 8) + x0;
+    P = tbig ? 0u : P * 0x01010101u;
     if (w == 0 || w == nword - 1) {  // real samples only
         const int lo_ = min(max(lead - 32 * w, 0), 32), hi_ = min(max(lead + n - 32 * w, 0), 32);
         const uint32_t mhi = hi_ >= 32 ? ~0u : ((1u << hi_) - 1u);
@@ -752,6 +735,7 @@ struct ClipStats {
     double mq, Mp, invM2;
     float invMf;
     int tpos, t0, nv;
+    int kneg;  // the clip holds a -32768 sample (r1_interior's paired squares may have wrapped)
 };
 __device__ __forceinline__ ClipStats clip_stats(const Shared *sh, int n, int L, int S, int do_vad)
 {
@@ -771,19 +755,16 @@ __device__ __forceinline__ ClipStats clip_stats(const Shared *sh, int n, int L, 
     s.invMf = uni(s.Mp > 0.0 ? (float)(1.0 / s.Mp) : 0.0f);  // as dsp_extract_general (same bits)
     s.invM2 = uni(s.Mp > 0.0 ? 1.0 / (s.Mp * s.Mp) : 0.0);   // endpoint energies (one rounding)
     s.nv = (do_vad && n >= L) ? (n - L) / S + 1 : 0;
+    s.kneg = kmin == -32768;
     return s;
 }
 
 // p90 order statistics of the VAD energies (:198) by ONE wave, nv <= 128: bitonic sort of the high
 // halves of the order-preserving keys; the rank's element is the one holding that high half, or,
 // when several do, the one of the right rank among them by the full key -> c.sh->pa / pb
-// p90 and the medians by a ballot radix select (wave_select2) instead of bitonic sorts: 70% of
-// the VALU of those phases, but three times the SALU, and the CU's scalar unit is shared by its 24
-// waves: 100k clips 2.64 -> 2.71 ms, 12.5k unchanged (profiles/r05rs_ab_select.txt).  1: both,
-// 2: p90 only, 0: neither
-#ifndef EXTRACT_SELECT_RADIX
-#define EXTRACT_SELECT_RADIX 0
-#endif
+// (a ballot radix select instead of the bitonic sorts, for p90 and the medians: 70% of the VALU of
+// those phases, but three times the SALU on the CU's shared scalar unit -- 100k clips 2.64 -> 2.71
+// ms, profiles/r05rs_ab_select.txt; removed)
 __device__ __forceinline__ void p90_select_wave(const Ctx &c, int nv, int lane)
 {
     const double vi = (double)(nv - 1) * 0.9;
@@ -798,14 +779,8 @@ __device__ __forceinline__ void p90_select_wave(const Ctx &c, int nv, int lane)
     const unsigned long long f1 = lane + 64 < nv ? dkey(c.vE[lane + 64]) : ~0ull;
     const unsigned h0 = (unsigned)(f0 >> 32), h1 = (unsigned)(f1 >> 32);
     unsigned a[2] = {h0, h1};
-    unsigned ka, kb;  // the high key words at ranks r0 and r1 (EXTRACT_SELECT_RADIX) ...
-    if (EXTRACT_SELECT_RADIX) {  // 1 or 2
-        wave_select2<2>(a, r0, ka, kb);
-    } else {  // ... or read from a bitonic sort of them
-        wave_bitonic<2>(a, lane);
-        ka = sorted_at<2>(a, r0);
-        kb = sorted_at<2>(a, r1);
-    }
+    wave_bitonic<2>(a, lane);
+    const unsigned ka = sorted_at<2>(a, r0), kb = sorted_at<2>(a, r1);  // the high key words at ranks r0, r1
     auto full_at = [&](int r) -> double {
         const unsigned kh = r == r0 ? ka : kb;  // never the pad's ~0u: r < nv
         const unsigned long long c0 = __ballot(h0 == kh), c1 = __ballot(h1 == kh);
@@ -899,11 +874,10 @@ __device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur
 // sits in the buffer and equal dsp_extract_general's.  Per sample y = w_j x (the reference's
 // windowed frame, :329-331), E += y^2, M += |y|; the weights of a vector's 8 samples are two
 // aligned 16-B reads from the window copy shifted by fs mod 4.  Returns F.
-#ifndef EXTRACT_R4_KV
-#define EXTRACT_R4_KV 7  // vectors per lane in one batch from L2: 7 (896 samples per row) leaves
-                         // the FAST kernel without VGPR spills; 9 (a whole 1102-sample frame)
-                         // 2.71 ms, 7 2.65 ms at 100k clips (profiles/r05s_ab_prefetch_kv.txt)
-#endif
+// vectors per lane in one batch from L2: 7 (896 samples per row) leaves the FAST kernel without
+// VGPR spills; 9 (a whole 1102-sample frame) 2.71 ms, 7 2.65 ms, 6 / 8 2.61-2.64 / 2.66-2.68 ms at
+// 100k clips (profiles/r05s_ab_prefetch_kv.txt, r05kv_ab_r4_batch.txt)
+static constexpr int R4_KV = 7;
 __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int L, int S,
                                          int st, int en, const ClipStats &cs, int j0, int j1, int wrank, int lane)
 {
@@ -935,7 +909,7 @@ __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, c
             canon_pair(w, canon_x2<NEAR0>(x8[2 * h], x8[2 * h + 1], cx), ea, m0, m1);
         }
     };
-    constexpr int KV = EXTRACT_R4_KV;
+    constexpr int KV = R4_KV;
     const int rl = lane & 15, row = lane >> 4;
     for (int gi = wrank; !(DSP_ABL & 1) && 4 * gi < F; gi += NWAVE) {
         const int g = 4 * gi + row;
@@ -1008,17 +982,7 @@ __device__ __forceinline__ void r5_fast(const Ctx &c, int F, float *featb, int w
         if (job < 3) {  // median by an in-wave bitonic sort
             unsigned a[2] = {in0 ? fkey(x0) : ~0u, in1 ? fkey(x1) : ~0u};
             float v0, v1;
-            if (EXTRACT_SELECT_RADIX == 1) {  // r1 = r0 or r0 + 1 < F
-                unsigned k0, k1;
-                if (F <= 64) {
-                    const unsigned b[1] = {a[0]};
-                    wave_select2<1>(b, r0, k0, k1);
-                } else {
-                    wave_select2<2>(a, r0, k0, k1);
-                }
-                v0 = fkey_value(k0);
-                v1 = fkey_value(r1 == r0 ? k0 : k1);
-            } else if (F <= 64) {
+            if (F <= 64) {
                 unsigned b[1] = {a[0]};
                 wave_bitonic<1>(b, lane);
                 v0 = fkey_value(sorted_at<1>(b, r0));
@@ -1064,25 +1028,17 @@ __device__ __forceinline__ void r5_fast(const Ctx &c, int F, float *featb, int w
 // than 64 clips per workgroup (12 500 clips: 0.506 -> 0.484 ms, a shorter tail; 100 000: 3.387
 // against 3.409 ms with 2; profiles/r04x_queue_chunk_ab.txt).  p.qchunk == 0 (at most two clips
 // per workgroup) or p.queue == NULL: the static split, no claims.  Thread 0 only.
-#ifndef EXTRACT_XCD_RANGES
-#define EXTRACT_XCD_RANGES 8  // 1: one range for every workgroup (A/B)
-#endif
-static_assert(EXTRACT_XCD_RANGES >= 1 && EXTRACT_XCD_RANGES <= 8, "queue_ws holds 8 range counters");
-// queue_ws word w of the layout lives at word w * EXTRACT_QSTRIDE: every counter on its own 256-B
+static constexpr int XCD_RANGES = 8;  // one per XCD (queue_ws holds 8 range counters)
+// queue_ws word w of the layout lives at word w * QSTRIDE: every counter on its own 256-B
 // line.  Agent-scope atomics on one line serialise (across the eight XCDs they go past the L2s),
 // and with all eight counters in one 64-B line the claims of 768 workgroups queued behind each
 // other: at 12 500 clips the clips that claimed late in the launch took up to 85 us (p99 73 us).
 // One line per counter: 12.5k clips 0.454-0.459 -> 0.436-0.440 ms (span p99 73 -> 35 us, workgroups
 // p50 402 -> 363 us), 100k 2.634-2.656 -> 2.616-2.621 ms (profiles/r05qs_ab_queue_lines.txt,
 // r05qs_stamps.txt).  Probing the other ranges with loads before claiming: 2.75 ms at 100k.
-#ifndef EXTRACT_QSTRIDE
-#define EXTRACT_QSTRIDE 64
-#endif
-#ifndef EXTRACT_STEAL_PROBE
-#define EXTRACT_STEAL_PROBE 0  // 1: probe other ranges' counters with loads before claiming (A/B)
-#endif
-static_assert(11 * EXTRACT_QSTRIDE * 4 <= DSP_QUEUE_WS_BYTES, "queue_ws too small for the counter layout");
-__device__ __forceinline__ unsigned *qword(unsigned *q, int w) { return q + w * EXTRACT_QSTRIDE; }
+static constexpr int QSTRIDE = 64;
+static_assert(11 * QSTRIDE * 4 <= DSP_QUEUE_WS_BYTES, "queue_ws too small for the counter layout");
+__device__ __forceinline__ unsigned *qword(unsigned *q, int w) { return q + w * QSTRIDE; }
 struct ClipQueue {  // wave-uniform; the mutable state lives in Shared (thread 0 only)
     unsigned *q;
     int B, nch, xcd, ch;
@@ -1128,18 +1084,18 @@ __device__ __forceinline__ unsigned queue_begin(const ClipQueue &Q, Shared *sh)
         sh->cdir = nx;
         return 0;
     }
-    if (sh->qrange >= EXTRACT_XCD_RANGES || Q.s0 == Q.nch) {  // every range exhausted, or none
+    if (sh->qrange >= XCD_RANGES || Q.s0 == Q.nch) {  // every range exhausted, or none
         sh->cdir = -1;
         return 0;
     }
-    const int y = (Q.xcd + sh->qrange) % EXTRACT_XCD_RANGES;
+    const int y = (Q.xcd + sh->qrange) % XCD_RANGES;
     sh->cy = y;
     sh->cdir = -2;
     return __hip_atomic_fetch_add(qword(Q.q, y), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ int queue_end(const ClipQueue &Q, Shared *sh, unsigned ret)
 {
-    constexpr int NR = EXTRACT_XCD_RANGES;
+    constexpr int NR = XCD_RANGES;
     if (sh->cdir != -2) return sh->cdir;
     int y = sh->cy;
     for (;;) {
@@ -1153,15 +1109,6 @@ __device__ __forceinline__ int queue_end(const ClipQueue &Q, Shared *sh, unsigne
         }
         // this range is used up: the next one (a blocking claim, rare: the end of the launch)
         int r = ++sh->qrange;
-#if EXTRACT_STEAL_PROBE
-        // ranges whose counters already show every chunk claimed are skipped on a load, not a claim
-        for (; r < NR; r++) {
-            const int yy = (Q.xcd + r) % NR;
-            const unsigned v = __hip_atomic_load(qword(Q.q, yy), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((unsigned)(Q.s0 + yy * D / NR) + v < (unsigned)(Q.s0 + (yy + 1) * D / NR)) break;
-        }
-        sh->qrange = r;
-#endif
         if (r >= NR) return -1;
         y = (Q.xcd + r) % NR;
         ret = __hip_atomic_fetch_add(qword(Q.q, y), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1197,22 +1144,17 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     Shared *sh = c.sh;
     // (the generic layout's and the exact redo's index arithmetic spills when hoisted: opaque
     // thread index there)
-#ifndef EXTRACT_OPAQUE_FAST
-#define EXTRACT_OPAQUE_FAST 0
-#endif
-    const int tid = (FAST && !EXACT && !EXTRACT_OPAQUE_FAST) ? (int)threadIdx.x : opaque_tid(), lane = tid & 63,
+    const int tid = (FAST && !EXACT) ? (int)threadIdx.x : opaque_tid(), lane = tid & 63,
               wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
     // frame sizes opaque per clip as well: constants derived from them ((double)L, ...) are
     // recomputed in the clip instead of being kept live across the loop
     int L = p.L, S = p.S;
-#ifndef EXTRACT_NO_OPAQUE_LS
     asm volatile("" : "+s"(L), "+s"(S));
-#endif
     const int n = cur.n, lead = cur.lead, nword = cur.nword;
     // outputs: the main kernel stages them in LDS (slot i mod EXTRACT_OSTAGE) and the workgroup
     // writes a chunk's clips together (flush_outputs); the exact redo writes them directly
     const int oslot = i & (EXTRACT_OSTAGE - 1);
-    float *featb = EXACT ? p.feat + (size_t)i * 15 : c.ofeat + 15 * oslot;
+    float *featb = EXACT ? out_feat(p, i) : reinterpret_cast<float *>(c.orow + DSP_OUT_ROW_WORDS * oslot);
     const int16_t *clip_g = p.pcm + cur.base + lead;  // the clip in global memory, sample coords
     STAMP(i, 0);
 #ifdef DSP_STAMPS
@@ -1249,12 +1191,11 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
         sh->schunk = -1;
         sh->sclear = 0;
     }
-#if EXTRACT_STATS_W0
     // wave 0 computes the clip statistics once and shares them (a second barrier), instead of
-    // every wave repeating the fp64 work
+    // every wave repeating the fp64 work (3.415 -> 3.386 ms at 100k clips, round 4)
     if (wid == 0) {
         const ClipStats c0 = clip_stats(sh, n, L, S, p.do_vad);
-        if (lane == 0) sh->cs = {c0.mq, c0.Mp, c0.invM2, c0.invMf, c0.tpos, c0.t0, c0.nv};
+        if (lane == 0) sh->cs = {c0.mq, c0.Mp, c0.invM2, c0.invMf, c0.tpos, c0.t0, c0.nv, c0.kneg};
     }
     __syncthreads();
     ClipStats cs;
@@ -1265,9 +1206,6 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     cs.tpos = uni(sh->cs.tpos);
     cs.t0 = uni(sh->cs.t0);
     cs.nv = uni(sh->cs.nv);
-#else
-    const ClipStats cs = clip_stats(sh, n, L, S, p.do_vad);
-#endif
     const double mq = cs.mq, Mp = cs.Mp;
     const int tpos = cs.tpos, t0 = cs.t0, nv = cs.nv;
     STAMP(i, 1);
@@ -1440,7 +1378,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     if constexpr (!EXACT)
         if (tid == 0) sh->next = resolve();  // claimed at the clip's start (-1: none)
     __syncthreads();
-    if constexpr (!EXACT && EXTRACT_PREFETCH) {
+    if constexpr (!EXACT) {
         // regs are dead since R2: the next clip's words load while R5 runs (unconditional, a
         // clip_none() reads zeros, so the compiler's vmcnt bookkeeping stays exact)
         const int nx = sh->next;
@@ -1508,15 +1446,16 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
         }
     if (tid == 0) {
         if constexpr (EXACT) {
-            p.start_end[2 * i] = st;
-            p.start_end[2 * i + 1] = en;
-            p.n_frames[i] = F;
-            p.status[i] = DSP_CLIP_OK | DSP_CLIP_FLAG_VAD_EXACT;
+            out_se(p, i)[0] = st;
+            out_se(p, i)[1] = en;
+            *out_nf(p, i) = F;
+            *out_st(p, i) = DSP_CLIP_OK | DSP_CLIP_FLAG_VAD_EXACT;
         } else {
-            c.ose[2 * oslot] = st;
-            c.ose[2 * oslot + 1] = en;
-            c.onf[oslot] = F;
-            c.ost[oslot] = DSP_CLIP_OK;
+            int32_t *orow = c.orow + DSP_OUT_ROW_WORDS * oslot;
+            orow[15] = st;
+            orow[16] = en;
+            orow[17] = F;
+            orow[18] = DSP_CLIP_OK;
             const int ch = i / EXTRACT_OSTAGE;  // the staged slots belong to chunk sh->schunk
             const unsigned m0 = sh->schunk == ch ? sh->smask : 0u;
             sh->schunk = ch;
@@ -1537,11 +1476,10 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
 // decisions so that R4 reads LDS and the registers take the next clip earlier -- from the
 // registers (16-way LDS bank conflicts on the copy) 3.78 ms, by LDS-DMA from L2 3.55 ms: R4 from LDS
 // took as long as from L2 (2.34 against 2.39 us per clip in the stamps; it is bound by its own
-// arithmetic), and the DMA's round trip sat on the critical path.
-#ifndef EXTRACT_FAST_PREFETCH
-#define EXTRACT_FAST_PREFETCH 0  // rows of the next clip's words loaded during R5 (the rest at its
-#endif                           // start): 1 row 3.52 ms, 2 rows 3.70 ms against 2.85 ms without, at
-                                 // 100k clips (spills; profiles/r05j_ab_prefetch_rows.txt)
+// arithmetic), and the DMA's round trip sat on the critical path.  Rows of the next clip's words
+// loaded during R5 (the rest at its start): 1 row 3.52 ms, 2 rows 3.70 ms against 2.85 ms without at
+// 100k clips (spills; profiles/r05j_ab_prefetch_rows.txt), and with 0 spills 2.65-2.68 against
+// 2.65 ms (r05s_ab_prefetch_kv.txt): not kept.
 
 // One clip, FAST layout, not the exact redo; its RREG words are already in flight into regs (word
 // r * NT + tid in regs[4r .. 4r+3]).  Endpoint energies from exact moments, decisions certified;
@@ -1559,7 +1497,7 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     asm volatile("" : "+s"(L), "+s"(S));  // per clip: constants derived from them are recomputed
     const int n = cur.n, lead = cur.lead, nword = cur.nword;
     const int oslot = i & (EXTRACT_OSTAGE - 1);
-    float *featb = c.ofeat + 15 * oslot;
+    float *featb = reinterpret_cast<float *>(c.orow + DSP_OUT_ROW_WORDS * oslot);
     STAMP(i, 0);
 #ifdef DSP_STAMPS
     if (p.stamps) {  // diagnostic build: the clip's loads landed (stamp 13; per wave: 24 + wave)
@@ -1589,7 +1527,7 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     MARK(stats);
     if (wid == 0) {  // the clip statistics once, shared through LDS
         const ClipStats c0 = clip_stats(sh, n, L, S, p.do_vad);
-        if (lane == 0) sh->cs = {c0.mq, c0.Mp, c0.invM2, c0.invMf, c0.tpos, c0.t0, c0.nv};
+        if (lane == 0) sh->cs = {c0.mq, c0.Mp, c0.invM2, c0.invMf, c0.tpos, c0.t0, c0.nv, c0.kneg};
     }
     __syncthreads();
     ClipStats cs;
@@ -1600,11 +1538,19 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     cs.tpos = uni(sh->cs.tpos);
     cs.t0 = uni(sh->cs.t0);
     cs.nv = uni(sh->cs.nv);
+    cs.kneg = uni(sh->cs.kneg);
     const int nv = cs.nv;
     STAMP(i, 1);
 
     // ---- R2: positive-sample bits, one 32-bit word per 32 buffer samples ---------------------
     MARK(R2);
+    if (cs.kneg) {  // rare: a -32768 sample may have wrapped r1_interior's paired squares
+#pragma unroll
+        for (int r = 0; r < RREG; r++) {
+            const int w = r * NT + tid;
+            if (w < nword && w > 0 && w < nword - 1) r1_redo_s2(&regs[4 * r], w, c.wS2);
+        }
+    }
     // then the partial word of the frame end this thread sums in pass A (one frame end per thread),
     // re-read from L2 and issued before the barrier so that it is in flight while the workgroup
     // synchronises.  Issued earlier, with the clip's words still live, it costs spills whose
@@ -1618,8 +1564,9 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     if (tid < 2) c.posw[nword + tid] = 0;
     MARK(paissue);
     short8 qa[4];
-    int pa_e0 = 0, pa_e1 = 0;
-    const int pa_w = vad_partial_issue(p, cur, L, S, nv, tid, qa, pa_e0, pa_e1);
+    int pa_e0 = 0, pa_e1 = 0, pa_w = -1;
+    if (64 * wid < 2 * nv)  // waves holding frame ends (2 nv <= 256: waves 0-3)
+        pa_w = vad_partial_issue(p, cur, L, S, nv, tid, qa, pa_e0, pa_e1);
     __syncthreads();
     STAMP(i, 2);
 
@@ -1657,7 +1604,7 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
             st = sh->n1 * S;              // :272
             en = min(sh->n6 * S + L, n);  // :273
         }
-        const ExtractParams &q = kargs(p);
+        const ExtractParams &q = p;
         if (q.vad_energy)
             for (int f = opaque_tid(); f < nv && f < q.ld_vad; f += NT) {
                 q.vad_energy[(size_t)i * q.ld_vad + f] = c.vE[f];
@@ -1671,10 +1618,6 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     const int F = r4_frames(p, c, cur, L, S, st, en, cs, sh->j0, sh->j1, wid, lane);
     STAMP(i, 12);
     __syncthreads();
-    if (EXTRACT_FAST_PREFETCH) {  // regs are dead: the next clip's first rows load while R5 runs
-        const int nx = sh->next;
-        issue_clip(regs, p, nx >= 0 ? clip_ref(p, nx) : clip_none(), opaque_tid(), 0, EXTRACT_FAST_PREFETCH);
-    }
     STAMP(i, 5);
 
     // ---- R5: 15-d statistics (compute_statistics x 3, fe.py:46-62) ------------------------
@@ -1689,7 +1632,7 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     }
     STAMP(i, 9);
     MARK(tail);
-    const ExtractParams &qs = kargs(p);
+    const ExtractParams &qs = p;
     if (qs.seq)
         for (int g = tid; g < F && g < qs.ld_seq; g += NT) {
             float *o = qs.seq + ((size_t)i * qs.ld_seq + g) * 3;
@@ -1698,10 +1641,11 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
             o[2] = (float)c.fZ[g];
         }
     if (tid == 0) {
-        c.ose[2 * oslot] = st;
-        c.ose[2 * oslot + 1] = en;
-        c.onf[oslot] = F;
-        c.ost[oslot] = DSP_CLIP_OK;
+        int32_t *orow = c.orow + DSP_OUT_ROW_WORDS * oslot;
+        orow[15] = st;
+        orow[16] = en;
+        orow[17] = F;
+        orow[18] = DSP_CLIP_OK;
         const int ch = i / EXTRACT_OSTAGE;  // the staged slots belong to chunk sh->schunk
         const unsigned m0 = sh->schunk == ch ? sh->smask : 0u;
         sh->schunk = ch;
@@ -1713,14 +1657,13 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
 
 __device__ __forceinline__ void write_bad_clip(const ExtractParams &p, int i, int tid)
 {
-    const ExtractParams &q = kargs(p);
-    if (tid < 15) q.feat[(size_t)i * 15 + tid] = __builtin_nanf("");
+    if (tid < 15) out_feat(p, i)[tid] = __builtin_nanf("");
     if (tid == 0) {
-        const int64_t nn = q.offsets[i + 1] - q.offsets[i];
-        q.status[i] = nn <= 0 ? DSP_CLIP_EMPTY : DSP_CLIP_TOO_LONG;
-        q.start_end[2 * i] = 0;
-        q.start_end[2 * i + 1] = 0;
-        q.n_frames[i] = 0;
+        const int64_t nn = p.offsets[i + 1] - p.offsets[i];
+        *out_st(p, i) = nn <= 0 ? DSP_CLIP_EMPTY : DSP_CLIP_TOO_LONG;
+        out_se(p, i)[0] = 0;
+        out_se(p, i)[1] = 0;
+        *out_nf(p, i) = 0;
     }
 }
 
@@ -1741,10 +1684,7 @@ __device__ __forceinline__ Ctx ctx_from(const ExtractCarve &cv, unsigned char *l
     c.rank = reinterpret_cast<int *>(lds + cv.rank);
     c.pS1 = reinterpret_cast<int *>(lds + cv.pS1);
     c.pS2 = reinterpret_cast<unsigned long long *>(lds + cv.pS2);
-    c.ofeat = reinterpret_cast<float *>(lds + cv.ost);
-    c.ose = reinterpret_cast<int32_t *>(lds + cv.ost + 4 * 15 * EXTRACT_OSTAGE);
-    c.onf = c.ose + 2 * EXTRACT_OSTAGE;
-    c.ost = c.onf + EXTRACT_OSTAGE;
+    c.orow = reinterpret_cast<int32_t *>(lds + cv.ost);
     c.total = 0;
     c.stamp_clip = 0;
     return c;
@@ -1806,22 +1746,27 @@ __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &
 }
 
 
-// the staged outputs of the chunk holding clip `done` (slots in sh->smask) to global memory,
-// contiguous per array: one clip's 76 B written on its own reach HBM as ~190 B of partial
-// sectors once L2 has evicted the lines between neighbouring clips' writes
+// the staged outputs of the chunk holding clip `done` (slots in sh->smask) to global memory: slot j
+// is one 19-word row in LDS (feat[15], start, end, n_frames, status), written as whole rows -- one
+// clip's 76 B written on its own reach HBM as ~190 B of partial sectors once L2 has evicted the
+// lines between neighbouring clips' writes; with the packed row layout (ostride 19, ABI 6) a
+// chunk's rows are one contiguous 304-B range
 __device__ __forceinline__ void flush_outputs(const ExtractParams &p, const Ctx &c, int done, int tid)
 {
-    const ExtractParams &q = kargs(p);
-    constexpr int CH = EXTRACT_OSTAGE;
+    constexpr int CH = EXTRACT_OSTAGE, RW = DSP_OUT_ROW_WORDS;
     const int cb = done & ~(CH - 1);
     // nothing staged for this chunk (its clips were deferred or bad: written directly) -> 0
     const unsigned m = c.sh->schunk == cb / CH ? c.sh->smask : 0u;
-    for (int t = tid; t < 15 * CH; t += NT)
-        if ((m >> (t / 15)) & 1) q.feat[(size_t)cb * 15 + t] = c.ofeat[t];
-    if (tid < 2 * CH && ((m >> (tid >> 1)) & 1)) q.start_end[2 * (size_t)cb + tid] = c.ose[tid];
-    if (tid < CH && ((m >> tid) & 1)) {
-        q.n_frames[cb + tid] = c.onf[tid];
-        q.status[cb + tid] = c.ost[tid];
+    if (tid < RW * CH) {
+        const int j = tid / RW, col = tid - RW * j;
+        if ((m >> j) & 1) {
+            const int32_t v = c.orow[tid];
+            int32_t *dst = col < 15   ? (int32_t *)out_feat(p, cb + j) + col
+                           : col < 17 ? out_se(p, cb + j) + (col - 15)
+                           : col == 17 ? out_nf(p, cb + j)
+                                       : out_st(p, cb + j);
+            *dst = v;
+        }
     }
 }
 
@@ -1850,17 +1795,15 @@ void extract_kernel(ExtractParams p)
     // queue_next returns below) is loaded before the window is built, so that its loads and the
     // window's round trip overlap (1 000 clips: 0.0558 -> 0.0533 ms per step; 12.5k and 100k
     // unchanged; profiles/r05pre_ab_first_clip.txt)
-    int pre = -1;
+    // FAST: a clip's loads are issued at the bottom of the previous trip (the first clip's here), on
+    // every path -- a clip_none() range when there is no clip or a bad one, whose loads read zeros --
+    // so the register array is never live across the loop's back edge (a path that skipped the issue
+    // left it live around the whole loop: 84 VGPR spills)
     if constexpr (FAST) {
         const int b = (int)blockIdx.x, ch = max(p.qchunk, 1);
         const int first = (p.qchunk > 0 && p.queue) ? (b < (p.B + ch - 1) / ch ? b * ch : -1) : (b < p.B ? b : -1);
-        if (first >= 0) {
-            const ClipRef c0 = clip_ref(p, first);
-            if (c0.ok) {
-                issue_clip(regs, p, c0, opaque_tid());
-                pre = first;
-            }
-        }
+        const ClipRef c0 = first >= 0 ? clip_ref(p, first) : clip_none();
+        issue_clip(regs, p, c0.ok ? c0 : clip_none(), opaque_tid());
     }
     build_window(p, c, tid, lane, wid);
     WG_CK(18);
@@ -1874,7 +1817,7 @@ void extract_kernel(ExtractParams p)
     }
     __syncthreads();
     WG_CK(19);
-    bool inflight = false;  // regs already hold clip i's loads (issued by the previous clip)
+    bool inflight = false;  // generic kernel: regs already hold clip i's loads (issued during the previous clip's R5)
     for (int i = sh->next; i >= 0;) {
         STAMP(i, 20);
 #ifdef DSP_STAMPS
@@ -1887,10 +1830,7 @@ void extract_kernel(ExtractParams p)
             write_bad_clip(p, i, opaque_tid());
             inflight = false;
         } else {
-            if (!inflight && i != pre)
-                issue_clip(regs, p, cur, opaque_tid());
-            else if (FAST && EXTRACT_FAST_PREFETCH < RREG)  // the rows not prefetched
-                issue_clip(regs, p, cur, opaque_tid(), EXTRACT_FAST_PREFETCH, RREG);
+            if (!FAST && !inflight) issue_clip(regs, p, cur, opaque_tid());
             unsigned cl = 0;
             if (tid == 0) cl = queue_begin(Q, sh);
             c.stamp_clip = i;
@@ -1903,11 +1843,10 @@ void extract_kernel(ExtractParams p)
                 if (!done && tid == 0) sh->next = queue_end(Q, sh, cl);  // a deferred clip returns before R4
             }
             if (!done && tid == 0) {
-                kargs(p).status[i] = DSP_CLIP_UNCERTIFIED;
-                if (kargs(p).queue) __hip_atomic_fetch_add(qword(kargs(p).queue, 9), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                *out_st(p, i) = DSP_CLIP_UNCERTIFIED;
+                if (p.queue) __hip_atomic_fetch_add(qword(p.queue, 9), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            inflight = (FAST ? EXTRACT_FAST_PREFETCH > 0 : EXTRACT_PREFETCH) && done;
-            pre = -1;
+            inflight = !FAST && done;
         }
         __syncthreads();  // LDS summaries are rewritten by the next clip; sh->next published
         STAMP(i, 14);
@@ -1916,6 +1855,13 @@ void extract_kernel(ExtractParams p)
         if (i < 0 || (i ^ prev) >= EXTRACT_OSTAGE) {  // next clip in another chunk
             flush_outputs(p, c, prev, opaque_tid());  // (addresses computed here, not hoisted and spilled)
             if (tid == 0) sh->sclear = 1;
+        }
+        if constexpr (FAST) {  // the next clip's loads (see the prologue), from a wave-uniform range
+            ClipRef nx = i < 0 ? clip_none() : sh->noff_for == i ? clip_ref_at(p, sh->noff[0], sh->noff[1]) : clip_ref(p, i);
+            if (!nx.ok) nx = clip_none();
+            nx.base = (int64_t)uni_u64((uint64_t)nx.base);  // (a per-lane value here made the compiler
+            nx.nvec = uni(nx.nvec);                          // waterfall every load over the lanes)
+            issue_clip(regs, p, nx, opaque_tid());
         }
         STAMP(prev, 15);
     }
@@ -1942,7 +1888,7 @@ __global__ __launch_bounds__(NT) void extract_exact_kernel(ExtractParams p)
     // the workgroup's clips blockIdx.x + G (t + NT k), NT statuses read at once, the near ties listed
     for (int64_t b0 = 0; b0 < p.B; b0 += (int64_t)gridDim.x * NT) {
         const int64_t i = b0 + blockIdx.x + (int64_t)gridDim.x * tid;
-        const bool tie = i < p.B && p.status[i] == DSP_CLIP_UNCERTIFIED;
+        const bool tie = i < p.B && *out_st(p, (int)i) == DSP_CLIP_UNCERTIFIED;
         if (tid == 0) sh->next = 0;
         __syncthreads();
         if (tie) list[atomicAdd(&sh->next, 1)] = (int)i;
@@ -1998,11 +1944,12 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
                                     int64_t max_len, int frame_length, int frame_shift,
                                     const double *window, int do_vad, double hi, double lo,
                                     double zr, float *feat, int32_t *start_end, int32_t *n_frames,
-                                    int32_t *status, double *vad_energy, int32_t *vad_zcr,
+                                    int32_t *status, int out_stride, double *vad_energy, int32_t *vad_zcr,
                                     int ld_vad, float *seq, int ld_seq, void *queue_ws, void *stream)
 {
     if (B < 0 || !offsets || !window || !feat || !start_end || !n_frames || !status)
         return DSP_ERR_ARGS;
+    if (out_stride != 0 && out_stride < DSP_OUT_ROW_WORDS) return DSP_ERR_ARGS;
     if (frame_length < 1 || frame_shift < 1 || max_len < 1) return DSP_ERR_ARGS;
     if (((uintptr_t)pcm & 15) != 0 || ((uintptr_t)queue_ws & 3) != 0) return DSP_ERR_ARGS;
     if ((vad_energy == nullptr) != (vad_zcr == nullptr)) return DSP_ERR_ARGS;
@@ -2043,6 +1990,7 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     p.start_end = start_end;
     p.n_frames = n_frames;
     p.status = status;
+    p.ostride = out_stride;
     p.vad_energy = vad_energy;
     p.vad_zcr = vad_zcr;
     p.ld_vad = ld_vad;

@@ -41,6 +41,7 @@ struct Params {
     double hi, lo, zr;
     float *feat;
     int32_t *start_end, *n_frames, *status;
+    int ostride;  // 0: per-array rows; > 0: row i of each output at i * ostride (ABI 6)
     double *vad_energy;
     int32_t *vad_zcr;
     int ld_vad;
@@ -50,6 +51,11 @@ struct Params {
     int64_t ws_stride;  // bytes per processed clip
     int64_t nvcap, fcap;
 };
+
+__device__ __forceinline__ float *out_feat(const Params &p, int i) { return p.feat + (int64_t)i * (p.ostride ? p.ostride : 15); }
+__device__ __forceinline__ int32_t *out_se(const Params &p, int i) { return p.start_end + (int64_t)i * (p.ostride ? p.ostride : 2); }
+__device__ __forceinline__ int32_t *out_nf(const Params &p, int i) { return p.n_frames + (int64_t)i * (p.ostride ? p.ostride : 1); }
+__device__ __forceinline__ int32_t *out_st(const Params &p, int i) { return p.status + (int64_t)i * (p.ostride ? p.ostride : 1); }
 
 // workspace of one clip: vE f64[nvcap], vZ i32[nvcap], fE f32[fcap], fM f32[fcap], fZ i32[fcap],
 // keys u64[max(nvcap, fcap)]
@@ -212,11 +218,11 @@ __device__ __forceinline__ void general_clip(const Params &p, Sh &s, const Ws &w
     // min_len == 0: this launch owns every clip, so an empty one (np.max of an empty array raises,
     // :72) and one longer than max_len are reported here; otherwise they belong to another launch
     if (p.min_len == 0 && (nn <= 0 || nn > p.max_len)) {
-        if (tid < 15) p.feat[(int64_t)i * 15 + tid] = __builtin_nanf("");
+        if (tid < 15) out_feat(p, i)[tid] = __builtin_nanf("");
         if (tid == 0) {
-            p.status[i] = nn <= 0 ? DSP_CLIP_EMPTY : DSP_CLIP_TOO_LONG;
-            p.start_end[2 * i] = p.start_end[2 * i + 1] = 0;
-            p.n_frames[i] = 0;
+            *out_st(p, i) = nn <= 0 ? DSP_CLIP_EMPTY : DSP_CLIP_TOO_LONG;
+            out_se(p, i)[0] = out_se(p, i)[1] = 0;
+            *out_nf(p, i) = 0;
         }
         return;
     }
@@ -424,7 +430,7 @@ __device__ __forceinline__ void general_clip(const Params &p, Sh &s, const Ws &w
     __syncthreads();
 
     // ---- statistics (fe.py:46-62): mean, population std, max, min, median -----------------
-    float *featb = p.feat + (int64_t)i * 15;
+    float *featb = out_feat(p, i);
     for (int q = 0; q < 3; q++) {
         auto get = [&](int64_t g) -> float { return q == 0 ? w.fE[g] : q == 1 ? w.fM[g] : (float)w.fZ[g]; };
         double sm = 0.0;
@@ -468,10 +474,10 @@ __device__ __forceinline__ void general_clip(const Params &p, Sh &s, const Ws &w
             o[2] = (float)w.fZ[g];
         }
     if (tid == 0) {
-        p.start_end[2 * i] = (int32_t)st;
-        p.start_end[2 * i + 1] = (int32_t)en;
-        p.n_frames[i] = (int32_t)F;
-        p.status[i] = DSP_CLIP_OK | flags;
+        out_se(p, i)[0] = (int32_t)st;
+        out_se(p, i)[1] = (int32_t)en;
+        *out_nf(p, i) = (int32_t)F;
+        *out_st(p, i) = DSP_CLIP_OK | flags;
     }
 }
 
@@ -506,12 +512,13 @@ extern "C" int dsp_extract_general(const void *pcm, int sample_bytes, const int6
                                    const int32_t *clip_index, int nclip, int64_t min_len, int64_t max_len,
                                    int frame_length, int frame_shift, const double *window, int do_vad,
                                    double hi, double lo, double zr, float *feat, int32_t *start_end,
-                                   int32_t *n_frames, int32_t *status, double *vad_energy,
+                                   int32_t *n_frames, int32_t *status, int out_stride, double *vad_energy,
                                    int32_t *vad_zcr, int ld_vad, float *seq, int ld_seq,
                                    void *workspace, size_t workspace_bytes, void *stream)
 {
     if (nclip < 0 || !pcm || !offsets || !window || !feat || !start_end || !n_frames || !status)
         return DSP_ERR_ARGS;
+    if (out_stride != 0 && out_stride < DSP_OUT_ROW_WORDS) return DSP_ERR_ARGS;
     if (sample_bytes != 2 && sample_bytes != 4) return DSP_ERR_ARGS;
     if (frame_length < 1 || frame_shift < 1 || max_len < 1 || min_len < 0) return DSP_ERR_ARGS;
     if (frame_length > (1 << 16) || max_len > ((int64_t)1 << 31)) return DSP_ERR_ARGS;
@@ -539,6 +546,7 @@ extern "C" int dsp_extract_general(const void *pcm, int sample_bytes, const int6
     p.start_end = start_end;
     p.n_frames = n_frames;
     p.status = status;
+    p.ostride = out_stride;
     p.vad_energy = vad_energy;
     p.vad_zcr = vad_zcr;
     p.ld_vad = ld_vad;

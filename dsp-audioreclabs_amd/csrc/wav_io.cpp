@@ -49,7 +49,10 @@ struct Fd {
 };
 
 // _parse_riff's walk: RIFF/WAVE, chunks padded to even sizes, 'fmt ' (WAVE_FORMAT_PCM, channels
-// and bits nonzero) before 'data', nframes = data size // frame size, the data fully present
+// and bits nonzero) before 'data', nframes = data size // frame size, the data fully present.
+// The walk is bounded by the RIFF chunk (8 + its size field) as well as by the file: the wave
+// module reads every subchunk through the RIFF chunk, so a RIFF size of 0 is "not a WAVE file"
+// and one that ends inside the data truncates the samples -- such files are left to it (kind 0).
 void scan_one(const char *path, int32_t &kind, int64_t &nsamp, int64_t &data_off)
 {
     kind = DSP_WAV_OTHER;
@@ -61,15 +64,18 @@ void scan_one(const char *path, int32_t &kind, int64_t &nsamp, int64_t &data_off
     const int64_t n = st.st_size;
     unsigned char h[16];
     if (n < 12 || !pread_all(f.fd, h, 12, 0) || std::memcmp(h, "RIFF", 4) || std::memcmp(h + 8, "WAVE", 4)) return;
+    const int64_t riff = le32(h + 4);
+    if (riff < 4) return;  // wave.open: 'not a WAVE file'
+    const int64_t lim = std::min<int64_t>(n, 8 + riff);
     int64_t p = 12;
     int ch = 0, sw = 0;
     bool fmt = false;
-    while (p + 8 <= n) {
+    while (p + 8 <= lim) {
         unsigned char c[8];
         if (!pread_all(f.fd, c, 8, p)) return;
         const int64_t size = le32(c + 4), body = p + 8;
         if (!std::memcmp(c, "fmt ", 4)) {
-            if (size < 16 || body + 16 > n || !pread_all(f.fd, h, 16, body)) return;
+            if (size < 16 || body + 16 > lim || !pread_all(f.fd, h, 16, body)) return;
             const uint32_t tag = le16(h), channels = le16(h + 2), bits = le16(h + 14);
             if (tag != 1 || channels == 0 || bits == 0) return;
             ch = (int)channels;
@@ -78,7 +84,7 @@ void scan_one(const char *path, int32_t &kind, int64_t &nsamp, int64_t &data_off
         } else if (!std::memcmp(c, "data", 4)) {
             if (!fmt) return;
             const int64_t frame = (int64_t)ch * sw, nbytes = size / frame * frame;
-            if (body + nbytes > n) return;  // truncated: the wave module's own behaviour (kind 0)
+            if (body + nbytes > lim) return;  // truncated (file or RIFF size): the wave module's own behaviour (kind 0)
             if (ch == 1 && (sw == 1 || sw == 2)) {
                 kind = sw == 2 ? DSP_WAV_S16_MONO : DSP_WAV_U8_MONO;
                 nsamp = nbytes / sw;

@@ -24,8 +24,9 @@ CLIP_NO_FRAMES = 3
 CLIP_TOO_LONG = 4
 CLIP_UNCERTIFIED = 5  # reserved (never produced)
 CLIP_FLAG_VAD_EXACT = 0x100
-ABI_VERSION = 5  # include/dsp_audiorec.h DSP_ABI_VERSION this binding is typed for
+ABI_VERSION = 6  # include/dsp_audiorec.h DSP_ABI_VERSION this binding is typed for
 QUEUE_WS_BYTES = 4096  # DSP_QUEUE_WS_BYTES
+OUT_ROW_WORDS = 19  # DSP_OUT_ROW_WORDS: feat[15] (f32), start, end, n_frames, status
 
 EXPORTS = ("dsp_extract_lds_bytes", "dsp_extract_features", "dsp_extract_general_workspace_bytes",
            "dsp_extract_general", "dsp_knn_workspace_bytes", "dsp_knn_workspace_fallbacks_offset",
@@ -60,9 +61,8 @@ def load_library(path=LIB_PATH):
     # the ABI version first: a stale library then fails with "rebuild it", not with a missing symbol
     L.dsp_abi_version.restype = i32
     L.dsp_abi_version.argtypes = []
-    # DSP_ABI_ANY=1: A/B tools loading an older variant library (tools/ab_bench.sh); the queue
-    # scratch this binding passes (4 KiB of zeros) serves the older layouts (8 or 64 bytes) too
-    if L.dsp_abi_version() != ABI_VERSION and not (os.environ.get("DSP_ABI_ANY") == "1" and L.dsp_abi_version() >= 2):
+    # DSP_ABI_ANY=1: A/B tools loading a variant library (tools/ab_bench.sh) built without an export
+    if L.dsp_abi_version() != ABI_VERSION:
         raise HipError("%s has ABI %d, this binding expects %d: rebuild it" % (path, L.dsp_abi_version(), ABI_VERSION))
     missing = [e for e in EXPORTS if not hasattr(L, e)]
     if missing and os.environ.get("DSP_ABI_ANY") != "1":
@@ -71,12 +71,12 @@ def load_library(path=LIB_PATH):
     L.dsp_extract_lds_bytes.argtypes = [i64, i32, i32]
     L.dsp_extract_features.restype = i32
     L.dsp_extract_features.argtypes = [vp, vp, i32, i64, i32, i32, vp, i32, dbl, dbl, dbl,
-                                       vp, vp, vp, vp, vp, vp, i32, vp, i32, vp, vp]
+                                       vp, vp, vp, vp, i32, vp, vp, i32, vp, i32, vp, vp]
     L.dsp_extract_general_workspace_bytes.restype = sz
     L.dsp_extract_general_workspace_bytes.argtypes = [i64, i64, i32, i32]
     L.dsp_extract_general.restype = i32
     L.dsp_extract_general.argtypes = [vp, i32, vp, vp, i32, i64, i64, i32, i32, vp, i32, dbl, dbl, dbl,
-                                      vp, vp, vp, vp, vp, vp, i32, vp, i32, vp, sz, vp]
+                                      vp, vp, vp, vp, i32, vp, vp, i32, vp, i32, vp, sz, vp]
     L.dsp_knn_workspace_bytes.restype = sz
     L.dsp_knn_workspace_bytes.argtypes = [i64, i64, i32, i32]
     if hasattr(L, "dsp_knn_workspace_fallbacks_offset") or os.environ.get("DSP_ABI_ANY") != "1":

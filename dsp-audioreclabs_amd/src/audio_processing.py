@@ -58,10 +58,16 @@ def _parse_riff(buf):
     """The data bytes and format of a well-formed PCM WAV image, exactly what wave.open +
     readframes(getnframes()) return for it (RIFF/WAVE header, chunks padded to even sizes, 'fmt '
     with WAVE_FORMAT_PCM before 'data', nframes = data size // frame size); None for anything
-    else -- the caller then takes the wave module itself, errors and all."""
+    else -- the caller then takes the wave module itself, errors and all.  The walk is bounded by
+    the RIFF chunk as well as the file: wave reads every subchunk through the RIFF chunk, so a RIFF
+    size below 4 is 'not a WAVE file' and a RIFF size ending inside the data truncates the samples;
+    such files go to the wave module."""
     if len(buf) < 12 or buf[0:4] != b"RIFF" or buf[8:12] != b"WAVE":
         return None
-    p, n, fmt = 12, len(buf), None
+    riff = int.from_bytes(buf[4:8], "little")
+    if riff < 4:
+        return None
+    p, n, fmt = 12, min(len(buf), 8 + riff), None
     while p + 8 <= n:
         cid, size = buf[p:p + 4], int.from_bytes(buf[p + 4:p + 8], "little")
         body = p + 8

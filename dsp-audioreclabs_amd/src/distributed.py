@@ -2,10 +2,12 @@
 
 Clips are independent, so rank r of P processes the contiguous block ``shard_range(B, r, P)``
 with no collective inside the step.  The only exchange is before KNN: every rank needs the
-whole [B, 15] feature matrix (and the per-clip endpoints, frame counts, status), gathered with
-ONE ``all_gather`` of a packed byte matrix -- RCCL over xGMI with the "nccl" backend, gloo on
-CPU in the tests.  Block sizes follow from ``shard_range`` on every rank, so no size exchange
-and no host sync precede the collective.  KNN then shards the queries and gathers the per-query
+whole [B, 15] feature matrix (and the per-clip endpoints, frame counts, status).  The extraction
+writes each clip's results as one packed 76-B row (``rows`` [B, 19] int32, ABI 6), so the exchange
+is ONE ``all_gather_into_tensor`` of those rows (``gather_rows``) -- no pack, pad or unpack
+kernels around it -- RCCL over xGMI with the "nccl" backend, gloo on CPU in the tests.  Block
+sizes follow from ``shard_range`` on every rank, so no size exchange and no host sync precede the
+collective.  KNN then shards the queries and gathers the per-query
 results (idx, dist, pred) the same way, again as one collective.
 """
 import math
@@ -80,6 +82,40 @@ def gather_packed(tensors, total, group=None):
     return _unpack_rows(full, layout)
 
 
+def gather_rows(rows, total, group=None):
+    """All-gather this rank's ``shard_range`` block of ``total`` packed result rows (``rows``
+    [n, W], contiguous) in rank order: ONE ``all_gather_into_tensor`` straight from the
+    extraction's own output buffer.  Returns [total, W] on every rank -- the collective's output
+    itself when the blocks are equal (every bench configuration: 100 000 clips over 1/2/4/8
+    ranks); ragged blocks are padded to the largest and cut back (two copies, off the bench path).
+    """
+    import torch
+    rank, ws = world()
+    if ws == 1:
+        return rows
+    sizes = [shard_range(total, r, ws) for r in range(ws)]
+    sizes = [hi - lo for lo, hi in sizes]
+    if rows.shape[0] != sizes[rank]:
+        raise ValueError("rank %d holds %d rows, its block is %d" % (rank, rows.shape[0], sizes[rank]))
+    m = max(sizes)
+    src = rows.contiguous()
+    if src.shape[0] < m:
+        src = torch.cat([src, src.new_zeros((m - src.shape[0],) + tuple(src.shape[1:]))])
+    out = src.new_empty((ws * m,) + tuple(src.shape[1:]))
+    dist.all_gather_into_tensor(out, src, group=group)
+    if all(s_ == m for s_ in sizes):
+        return out
+    return torch.cat([out[r * m:r * m + sizes[r]] for r in range(ws)])
+
+
+def result_views(rows):
+    """The per-array results as views of packed rows [B, 19] (the layout of FeatureExtractor's
+    ``rows``: feat[15] as f32 bits, start, end, n_frames, status)."""
+    import torch
+    return dict(rows=rows, feat=rows.view(torch.float32)[:, :15], start_end=rows[:, 15:17],
+                n_frames=rows[:, 17], status=rows[:, 18])
+
+
 def all_gather_rows(x, total=None, group=None):
     """Concatenate every rank's rows (in rank order) on every rank.
 
@@ -107,13 +143,20 @@ def all_gather_rows(x, total=None, group=None):
 def extract_sharded(extract_fn, make_shard, total):
     """Run ``extract_fn(make_shard(lo, hi))`` on this rank's block and gather the results.
 
-    ``extract_fn`` returns a dict of row-major tensors (feat, start_end, n_frames, status ...);
-    all of them travel in one packed all-gather, so each rank ends with the full-batch dict.
+    ``extract_fn`` returns FeatureExtractor's dict: its packed ``rows`` travel in one
+    ``gather_rows`` collective and the per-array results come back as views of the gathered rows;
+    any other row-major tensors (vad lists, sequences) in one more packed all-gather.
     """
     rank, ws = world()
     lo, hi = shard_range(total, rank, ws)
     out = extract_fn(make_shard(lo, hi))
-    return gather_packed(out, total)
+    if "rows" not in out:
+        return gather_packed(out, total)
+    res = result_views(gather_rows(out["rows"], total))
+    rest = {k: v for k, v in out.items() if k not in res}
+    if rest:
+        res.update(gather_packed(rest, total))
+    return res
 
 
 def knn_sharded(knn_fn, ref, labels, queries, k, self_query=False):

@@ -55,12 +55,17 @@ class FeatureExtractor:
         self._bufs = {}
 
     def _queue_ws(self):
-        """The zeroed DSP_QUEUE_WS_BYTES scratch of this extractor's launches (stream-ordered
-        reuse: one extractor is not meant to launch on two streams at once)."""
+        """The zeroed DSP_QUEUE_WS_BYTES scratch of this extractor's launches on the CURRENT
+        stream.  Launches on one stream are ordered, so they share one buffer (each launch leaves
+        it zeroed); a launch on another stream -- including a HIP-graph capture, whose replays
+        may overlap eager calls -- gets its own, so two launches can never claim chunks from the
+        same counters."""
         import torch
-        q = getattr(self, "_queue", None)
+        qs = self.__dict__.setdefault("_queues", {})
+        key = torch.cuda.current_stream(self.device).cuda_stream
+        q = qs.get(key)
         if q is None:
-            q = self._queue = torch.zeros(_hip.QUEUE_WS_BYTES // 4, dtype=torch.int32, device=self.device)
+            q = qs[key] = torch.zeros(_hip.QUEUE_WS_BYTES // 4, dtype=torch.int32, device=self.device)
         return q
 
     def lds_bytes(self, max_len):
@@ -71,10 +76,12 @@ class FeatureExtractor:
         key = (B, max_len)
         if key not in self._bufs:
             d = self.device
-            o = dict(feat=torch.empty((B, 15), dtype=torch.float32, device=d),
-                     start_end=torch.empty((B, 2), dtype=torch.int32, device=d),
-                     n_frames=torch.empty(B, dtype=torch.int32, device=d),
-                     status=torch.empty(B, dtype=torch.int32, device=d))
+            # one packed row per clip (DSP_OUT_ROW_WORDS int32 words: feat[15] as f32 bits, start,
+            # end, n_frames, status), written by the kernels with out_stride = 19; the four result
+            # arrays are strided views of it, and "rows" travels in one collective unpacked
+            rows = torch.empty((B, _hip.OUT_ROW_WORDS), dtype=torch.int32, device=d)
+            o = dict(rows=rows, feat=rows.view(torch.float32)[:, :15], start_end=rows[:, 15:17],
+                     n_frames=rows[:, 17], status=rows[:, 18])
             if self.return_vad_lists:
                 ld = max(1, (max_len - self.L) // self.S + 1) if max_len >= self.L else 1
                 o["vad_energy"] = torch.zeros((B, ld), dtype=torch.float64, device=d)
@@ -107,8 +114,9 @@ class FeatureExtractor:
         DSP_CLIP_TOO_LONG); without it, device-tensor offsets cost one host sync (the longest
         clip sizes the launch), so pass ``max_len`` to capture the call in a HIP graph.  Returns a
         dict of device tensors: feat [B,15] f32, start_end [B,2] i32, n_frames [B] i32, status
-        [B] i32 (+ vad_energy/vad_zcr, seq when requested).  The tensors are reused by the next
-        call with the same shape.
+        [B] i32 -- strided views of ``rows`` [B,19] i32, each clip's packed 76-B record -- (+
+        vad_energy/vad_zcr, seq when requested).  The tensors are reused by the next call with the
+        same shape.
         """
         import torch
         d = self.device
@@ -146,8 +154,8 @@ class FeatureExtractor:
         if sq is not None:
             lds_ = sq.shape[1]
         args = (int(self.do_vad), hi, lo, zr, _hip.ptr(out["feat"]), _hip.ptr(out["start_end"]),
-                _hip.ptr(out["n_frames"]), _hip.ptr(out["status"]), _hip.ptr(ve), _hip.ptr(vz), ldv,
-                _hip.ptr(sq), lds_)
+                _hip.ptr(out["n_frames"]), _hip.ptr(out["status"]), _hip.OUT_ROW_WORDS, _hip.ptr(ve),
+                _hip.ptr(vz), ldv, _hip.ptr(sq), lds_)
         cap = 0 if wide else self.fused_cap()
         if not wide and B > 0 and cap > 0:
             # the clip-queue scratch: zeroed once, and every launch leaves it zeroed again (the

@@ -30,10 +30,11 @@
 extern "C" {
 #endif
 
-#define DSP_ABI_VERSION 5  /* 2: dsp_extract_features takes the clip-queue scratch (queue_ws);
+#define DSP_ABI_VERSION 6  /* 2: dsp_extract_features takes the clip-queue scratch (queue_ws);
                               3: queue_ws is 64 bytes (per-XCD chunk counters);
                               4: the batch WAV reader (dsp_wav_scan / dsp_wav_read);
-                              5: queue_ws is 4 KiB (each counter on its own 256-B line) */
+                              5: queue_ws is 4 KiB (each counter on its own 256-B line);
+                              6: the extraction entry points take out_stride (packed result rows) */
 
 /* return codes */
 #define DSP_OK 0
@@ -43,6 +44,8 @@ extern "C" {
 #define DSP_ERR_HIP 1000      /* + hipError_t of the failed launch */
 
 #define DSP_QUEUE_WS_BYTES 4096  /* dsp_extract_features' queue_ws */
+#define DSP_OUT_ROW_WORDS 19     /* one clip's results as a packed row of 4-byte words: feat[15] (f32),
+                                    start, end, n_frames, status (int32) -- 76 B */
 
 /* per-clip status[b] (low byte) -- same codes as the oracle */
 #define DSP_CLIP_OK 0
@@ -92,6 +95,11 @@ size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int frame_shift)
  * start_end int32 [B,2]: start_point / end_point (0, len when do_vad == 0).
  * n_frames  int32 [B]: metadata['n_frames'] (frames after the crop).
  * status    int32 [B]: DSP_CLIP_* | flags.
+ * out_stride 0: the four arrays above, each row-major as given.  >= DSP_OUT_ROW_WORDS: row b of
+ *           each output starts b * out_stride 4-byte words after its pointer -- one packed row
+ *           buffer rows[B][19] is feat = rows, start_end = rows + 15, n_frames = rows + 17, status
+ *           = rows + 18, out_stride = 19: each clip's 76-B record is contiguous, so the per-clip
+ *           results of a shard travel in one collective without packing.
  * vad_energy/vad_zcr (optional, may be NULL): float64 / int32 [B, ld_vad]: metadata energy_list,
  *           zcr_list (first (len-L)//S+1 entries; rows of clips with len < L are untouched).
  * seq       (optional, may be NULL): float32 [B, ld_seq, 3] per-frame (E, M, ZCR) -- the
@@ -108,7 +116,7 @@ size_t dsp_extract_lds_bytes(int64_t max_len, int frame_length, int frame_shift)
 int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, int B, int64_t max_len,
                          int frame_length, int frame_shift, const double *window, int do_vad,
                          double hi, double lo, double zr, float *feat, int32_t *start_end,
-                         int32_t *n_frames, int32_t *status, double *vad_energy,
+                         int32_t *n_frames, int32_t *status, int out_stride, double *vad_energy,
                          int32_t *vad_zcr, int ld_vad, float *seq, int ld_seq, void *queue_ws,
                          void *stream);
 
@@ -134,8 +142,8 @@ int dsp_extract_general(const void *pcm, int sample_bytes, const int64_t *offset
                         const int32_t *clip_index, int nclip, int64_t min_len, int64_t max_len,
                         int frame_length, int frame_shift, const double *window, int do_vad,
                         double hi, double lo, double zr, float *feat, int32_t *start_end,
-                        int32_t *n_frames, int32_t *status, double *vad_energy, int32_t *vad_zcr,
-                        int ld_vad, float *seq, int ld_seq, void *workspace,
+                        int32_t *n_frames, int32_t *status, int out_stride, double *vad_energy,
+                        int32_t *vad_zcr, int ld_vad, float *seq, int ld_seq, void *workspace,
                         size_t workspace_bytes, void *stream);
 
 /*

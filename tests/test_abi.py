@@ -58,13 +58,15 @@ def test_host_argument_checks(lib):
     buf = ctypes.create_string_buffer(64)
     p = ctypes.cast(buf, ctypes.c_void_p)
     p2 = ctypes.c_void_p(p.value + 2)  # misaligned pcm
-    args = lambda pcm, B, L=1102, S=441, feat=p, q=None: (pcm, p, B, 44100, L, S, p, 1, 0.5, 0.1, 1.5,
-                                                         feat, p, p, p, None, None, 0, None, 0, q, None)
+    args = lambda pcm, B, L=1102, S=441, feat=p, q=None, os_=0: (pcm, p, B, 44100, L, S, p, 1, 0.5, 0.1, 1.5,
+                                                                 feat, p, p, p, os_, None, None, 0, None, 0, q, None)
     assert f(*args(p, -1)) == _hip.DSP_ERR_ARGS
     assert f(*args(p, 4, feat=None)) == _hip.DSP_ERR_ARGS
     assert f(*args(p2, 4)) == _hip.DSP_ERR_ARGS
     assert f(*args(p, 4, L=0)) == _hip.DSP_ERR_ARGS
     assert f(*args(p, 4, q=p2)) == _hip.DSP_ERR_ARGS  # misaligned clip-queue scratch
+    assert f(*args(p, 4, os_=18)) == _hip.DSP_ERR_ARGS  # a result row needs DSP_OUT_ROW_WORDS words
+    assert f(*args(p, 0, os_=19)) == _hip.DSP_OK
     assert f(*args(p, 0)) == _hip.DSP_OK  # empty batch: nothing to launch
     assert lib.dsp_knn_workspace_bytes(100, 100, 4097, 5) == 0
     assert lib.dsp_knn_workspace_bytes(100, 100, 33, 5) > 0  # high-dimensional screen
@@ -77,7 +79,7 @@ def test_host_argument_checks(lib):
     assert lib.dsp_zscore_fit(None, 10, 15, p, p, None) == _hip.DSP_ERR_ARGS
     g = lib.dsp_extract_general
     gargs = lambda sb=2, ws=None, nws=0, n=4: (p, sb, p, None, n, 0, 44100, 1102, 441, p, 1, 0.5, 0.1, 1.5,
-                                              p, p, p, p, None, None, 0, None, 0, ws, nws, None)
+                                              p, p, p, p, 0, None, None, 0, None, 0, ws, nws, None)
     assert g(*gargs(sb=3)) == _hip.DSP_ERR_ARGS
     assert g(*gargs()) == _hip.DSP_ERR_WORKSPACE
     assert g(*gargs(n=0)) == _hip.DSP_OK

@@ -47,7 +47,20 @@ def _worker(rank, ws, port, out_dir):
             return {"feat": torch.as_tensor(r["feat"]), "start_end": torch.as_tensor(r["start_end"]),
                     "n_frames": torch.as_tensor(r["n_frames"])}
 
+        def extract_rows(pcm):
+            # FeatureExtractor's output layout: packed [n, 19] int32 rows and views of them
+            r = extract(pcm)
+            n = r["feat"].shape[0]
+            rows = torch.zeros((n, 19), dtype=torch.int32)
+            rows.view(torch.float32)[:, :15] = r["feat"].to(torch.float32)
+            rows[:, 15:17] = r["start_end"].to(torch.int32)
+            rows[:, 17] = r["n_frames"].to(torch.int32)
+            return D.result_views(rows)
+
         got = D.extract_sharded(extract, make_shard, B)
+        # packed rows: one all_gather_into_tensor, ragged (13 = 7 + 6), equal (16 = 8 + 8) and an
+        # empty block (1 = 1 + 0)
+        rows_r = {b: D.extract_sharded(extract_rows, make_shard, b) for b in (B, 16, 1)}
         labels = torch.arange(B, dtype=torch.int32) % 3
         X = got["feat"].to(torch.float64).numpy()
 
@@ -65,7 +78,8 @@ def _worker(rank, ws, port, out_dir):
         np.savez(os.path.join(out_dir, "rank%d.npz" % rank), feat=got["feat"].numpy(),
                  start_end=got["start_end"].numpy(), n_frames=got["n_frames"].numpy(),
                  idx=idx.numpy(), dist=dist_.numpy(), pred=pred.numpy(), one_feat=one["feat"].numpy(),
-                 one_n=one["n_frames"].numpy(), i1=i1.numpy(), d1=d1.numpy(), p1=p1.numpy())
+                 one_n=one["n_frames"].numpy(), i1=i1.numpy(), d1=d1.numpy(), p1=p1.numpy(),
+                 **{"rows%d_%s" % (b, k): v.numpy() for b, g in rows_r.items() for k, v in g.items()})
     finally:
         dist.destroy_process_group()
 
@@ -93,3 +107,11 @@ def test_gloo_world2_shard_gather(tmp_path):
         assert np.array_equal(got["one_feat"], full["feat"][:1]) and np.array_equal(got["one_n"], full["n_frames"][:1])
         i1, d1, p1 = oracle.knn(full["feat"].astype(np.float64), y, full["feat"][:1].astype(np.float64), 3, n_classes=3)
         assert np.array_equal(got["i1"], i1) and np.array_equal(got["d1"], d1) and np.array_equal(got["p1"], p1)
+        for b in (B, 16, 1):  # gather_rows: every rank holds every clip's packed row, in order
+            fb = oracle.process_batch(make_batch(b, base_seed=11, n_samples=8000).reshape(-1),
+                                      np.arange(b + 1, dtype=np.int64) * 8000, L, S, create_window("hamming", L))
+            assert got["rows%d_rows" % b].shape == (b, 19)
+            assert np.array_equal(got["rows%d_feat" % b], fb["feat"].astype(np.float32))
+            assert np.array_equal(got["rows%d_start_end" % b], fb["start_end"])
+            assert np.array_equal(got["rows%d_n_frames" % b], fb["n_frames"])
+            assert not got["rows%d_status" % b].any()

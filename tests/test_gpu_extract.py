@@ -36,7 +36,7 @@ def packed(golden):
 def test_library_and_device():
     from src import _hip
     L = _hip.load_library()
-    assert L.dsp_abi_version() == _hip.ABI_VERSION == 5
+    assert L.dsp_abi_version() == _hip.ABI_VERSION == 6
     _hip.require_device()
 
 

@@ -89,7 +89,7 @@ def _general(pcm, off, L, S, win, vad=True, sample_bytes=2, nv_ld=None):
     ws = torch.empty(nb, dtype=torch.uint8, device=d)
     P = _hip.ptr
     rc = lib.dsp_extract_general(P(t), sample_bytes, P(o), None, B, 0, ml, L, S, P(w), int(vad), 0.5, 0.1, 1.5,
-                                 P(out["feat"]), P(out["start_end"]), P(out["n_frames"]), P(out["status"]),
+                                 P(out["feat"]), P(out["start_end"]), P(out["n_frames"]), P(out["status"]), 0,
                                  P(out["vad_energy"]), P(out["vad_zcr"]), ld, P(out["seq"]), ldf, P(ws), nb,
                                  _hip.stream_handle(d))
     _hip.check(rc, "dsp_extract_general")

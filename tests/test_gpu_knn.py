@@ -251,3 +251,35 @@ def test_knn_kc6_duplicates_and_ties_fall_back_exactly():
     assert np.array_equal(i1.cpu().numpy(), i0) and np.array_equal(d1.cpu().numpy(), d0)
     assert np.array_equal(p1.cpu().numpy(), p0)
     assert st["fallbacks"] > 0, st
+
+
+def test_knn_on_extracted_features_20k():
+    """configs[4] on extracted features, as the reference chains them
+    (experiments/run_experiments.py:262-280, src/models.py:33-35): 20 000 synthetic utterances
+    through the fused extraction, normalize_features on the device, then the exact k = 5
+    self-query over all 20 000 z-scored 15-d vectors.  Extracted features are the hard case for
+    the fp32 screen (integer ZCR statistics, correlated columns, near duplicates): whatever the
+    fallback count, a contiguous block of 2 000 queries and the z-score statistics must equal the
+    oracle bit for bit."""
+    import torch
+    from src.pipeline import FeatureExtractor, knn_classify, zscore_apply, zscore_fit
+    from src.synth import make_batch_device
+    n, k = 20000, 5
+    x = make_batch_device(n, "cuda", base_seed=21)
+    out = FeatureExtractor(1102, 441, "hamming", True)(x)
+    assert not (out["status"] & 0xFF).any().item()
+    feat = out["feat"].to(torch.float64)
+    mu, sd = zscore_fit(feat)
+    m0, s0 = oracle.zscore_fit(feat.cpu().numpy())
+    assert np.array_equal(mu.cpu().numpy(), m0) and np.array_equal(sd.cpu().numpy(), np.where(s0 == 0, 1, s0))
+    X = zscore_apply(feat, mu, sd)
+    y = (torch.arange(n, device="cuda") % 10).to(torch.int32)
+    st = {}
+    idx, dist, pred = knn_classify(X, y, X, k, self_offset=0, n_classes=10, stats=st)
+    Xh, yh = X.cpu().numpy(), y.cpu().numpy()
+    lo = 9000
+    i0, d0, p0 = oracle.knn(Xh, yh, Xh[lo:lo + 2000], k, n_classes=10, self_offset=lo, nthreads=16)
+    assert np.array_equal(idx.cpu().numpy()[lo:lo + 2000], i0), st
+    assert np.array_equal(dist.cpu().numpy()[lo:lo + 2000], d0), st
+    assert np.array_equal(pred.cpu().numpy()[lo:lo + 2000], p0), st
+    print("extracted-feature KNN: %d of %d queries fell back to the exhaustive fp64 scan" % (st["fallbacks"], n))

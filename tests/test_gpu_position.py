@@ -114,9 +114,10 @@ def test_sharded_extraction_odd_shard_size():
 
 
 def test_two_streams_concurrent_and_static_split():
-    """Two extractions in flight at once on two streams (each call has its own clip-queue
-    scratch), and the C ABI's static split (queue_ws = NULL): every result equals the oracle /
-    the queued launch bit for bit."""
+    """Two extractions in flight at once on two streams -- two extractors, and ONE extractor
+    launching on both streams with no sync in between (its clip-queue scratch is per stream, so
+    neither launch can claim the other's chunks) -- and the C ABI's static split (queue_ws =
+    NULL): every result equals the oracle / the queued launch bit for bit."""
     import torch
     from src import _hip
     from src.pipeline import FeatureExtractor, create_window
@@ -138,22 +139,36 @@ def test_two_streams_concurrent_and_static_split():
         for k in ref_a:
             assert torch.equal(oa[k], ref_a[k]), k
             assert torch.equal(ob[k], ref_b[k]), k
+    # one extractor, two streams, batches of two sizes (separate output buffers) in flight at once
+    xc = xa[:2300].contiguous()
+    ref_c = {k: v.clone() for k, v in fa(xc).items()}
+    for _ in range(5):
+        with torch.cuda.stream(sa):
+            oa = fa(xa)
+        with torch.cuda.stream(sb):
+            oc = fa(xc)
+        torch.cuda.synchronize()
+        for k in ref_a:
+            assert torch.equal(oa[k], ref_a[k]), k
+            assert torch.equal(oc[k], ref_c[k]), k
+    for k in ref_c:
+        assert torch.equal(ref_c[k], ref_a[k][:2300]), k
     host = xa.cpu().numpy()
     for i in range(0, 3000, 211):
         r = oracle.process_clip(host[i], L, S, create_window("hamming", L))
         assert tuple(ref_a["start_end"][i].tolist()) == (r["start"], r["end"])
         assert not feat_close(ref_a["feat"][i].cpu().numpy(), r["feat"]).any()
-    # queue_ws = NULL: the static split, same bits
-    out = {k: torch.empty_like(v) for k, v in ref_a.items()}
+    # queue_ws = NULL: the static split, same bits, into four separate arrays (out_stride 0)
+    out = {k: torch.empty_like(v) for k, v in ref_a.items() if k != "rows"}
     flat = xa.reshape(-1)
     off = torch.arange(3001, dtype=torch.int64, device="cuda") * xa.shape[1]
     P = _hip.ptr
     rc = _hip.lib().dsp_extract_features(P(flat), P(off), 3000, xa.shape[1], L, S, P(fa.window), 1, 0.5, 0.1, 1.5,
                                          P(out["feat"]), P(out["start_end"]), P(out["n_frames"]), P(out["status"]),
-                                         None, None, 0, None, 0, None, _hip.stream_handle())
+                                         0, None, None, 0, None, 0, None, _hip.stream_handle())
     _hip.check(rc, "dsp_extract_features")
     torch.cuda.synchronize()
-    for k in ref_a:
+    for k in out:
         assert torch.equal(out[k], ref_a[k]), k
 
 
@@ -170,14 +185,14 @@ def test_queue_modes_same_bits():
     for B in (1000, 1400, 4000):
         x = torch.as_tensor(make_batch(B, base_seed=900 + B)).cuda()
         ref = {k: v.clone() for k, v in fx(x).items()}
-        out = {k: torch.empty_like(v) for k, v in ref.items()}
+        out = {k: torch.empty_like(v) for k, v in ref.items() if k != "rows"}
         flat = x.reshape(-1)
         off = torch.arange(B + 1, dtype=torch.int64, device="cuda") * x.shape[1]
         P = _hip.ptr
         rc = _hip.lib().dsp_extract_features(P(flat), P(off), B, x.shape[1], L, S, P(fx.window), 1, 0.5, 0.1, 1.5,
                                              P(out["feat"]), P(out["start_end"]), P(out["n_frames"]),
-                                             P(out["status"]), None, None, 0, None, 0, None, _hip.stream_handle())
+                                             P(out["status"]), 0, None, None, 0, None, 0, None, _hip.stream_handle())
         _hip.check(rc, "dsp_extract_features")
         torch.cuda.synchronize()
-        for k in ref:
+        for k in out:
             assert torch.equal(out[k], ref[k]), (B, k)

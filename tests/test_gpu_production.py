@@ -1,10 +1,10 @@
 """GPU parity at production batch sizes: the persistent multi-clip loop the benchmark times.
 
-The extraction grid is persistent (two workgroups per CU, 512 on MI355X): workgroup w takes clip
-w, then claims clips from a launch-wide queue; these tests launch far more clips than workgroups,
-so every workgroup processes many clips in sequence (LDS summaries reused, the next clip's loads
-issued before R5, near-tie redo list holding several clips), and compare everything with the C
-oracle (reference algorithm:
+The extraction grid is persistent (three workgroups per CU, 768 on MI355X): workgroup w takes its
+first chunk of clips by its own index, then claims chunks from a launch-wide queue; these tests
+launch far more clips than workgroups, so every workgroup processes many clips in sequence (LDS
+summaries and output staging reused, several near ties deferred to the exact kernel), and compare
+everything with the C oracle (reference algorithm:
 src/audio_processing.py:336-396, src/feature_extraction.py:12-88).  They also simulate the
 8-rank sharding of BASELINE configs[3]/[4] on one GPU: shards processed
 separately and concatenated must equal the single launch.
@@ -22,6 +22,12 @@ from test_gpu_extract import feat_close
 pytestmark = pytest.mark.gpu
 
 L, S = 1102, 441
+
+
+def grid():
+    """The fused kernel's persistent grid: EXTRACT_WG_PER_CU (3) workgroups per CU."""
+    import torch
+    return 3 * torch.cuda.get_device_properties(0).multi_processor_count
 
 
 def near_tie_clip(n=44100, A=3000):
@@ -58,20 +64,22 @@ def _check(out, clips, w, vad=True, idx=None):
 
 def test_production_batch_2000_ragged_and_near_ties():
     """2000 clips of BASELINE configs[1] (Hamming, 1102/441, VAD) with empty, short, ragged and
-    near-tie clips scattered; four near-tie clips G apart (round 1's static split put them in one
-    workgroup's redo list; the queue spreads them by claim order)."""
+    near-tie clips scattered; four near-tie clips G / 2 apart in the first chunks of four different
+    workgroups (round 1's static split put such clips in one workgroup's redo list)."""
     import torch
     from src.pipeline import FeatureExtractor, create_window
     from src.synth import make_batch
     B = 2000
-    G = 2 * torch.cuda.get_device_properties(0).multi_processor_count  # persistent grid
+    G = grid()
+    ties = [3 + j * (G // 2) for j in range(4)]
+    assert ties[-1] < B
     base = make_batch(B, base_seed=500)
     clips = [base[i] for i in range(B)]
     rng = np.random.default_rng(5)
     for i in rng.choice(B, 60, replace=False):  # ragged / short / degenerate lengths
         n = int(rng.choice([0, 1, 7, 500, 1101, 1102, 1103, 2000, 9000, 30001, 44099]))
         clips[i] = clips[i][:n].copy()
-    for i in (3, 3 + G, 3 + 2 * G, 3 + 3 * G):
+    for i in ties:
         clips[i] = near_tie_clip()
     clips[17] = np.zeros(44100, np.int16)  # silence: no high-energy frame
     off = np.zeros(B + 1, np.int64)
@@ -81,7 +89,7 @@ def test_production_batch_2000_ragged_and_near_ties():
     out = {k: v.cpu().numpy() for k, v in fx(torch.as_tensor(pcm).cuda(), off).items()}
     _check(out, clips, create_window("hamming", L))
     redo = (out["status"] >> 8) & 1
-    assert redo[[3, 3 + G, 3 + 2 * G, 3 + 3 * G]].all(), "near ties were not redone exactly"
+    assert redo[ties].all(), "near ties were not redone exactly"
 
 
 @pytest.mark.parametrize("win", ["hamming", "hanning", "rectangular"])
@@ -102,12 +110,13 @@ def test_production_12500_per_rank_batch(win):
 
 
 def test_large_batch_one_launch():
-    """More clips than the persistent grid's slots x 256 (the round-3 launch-chunking boundary, now
-    one launch): clips on both sides of the old boundary and at the end match the oracle."""
+    """More clips than the persistent grid's slots x 256 in one launch (round 3 chunked launches at
+    that boundary; the clip queue's chunk counters now run far past it): clips on both sides of it
+    and at the end match the oracle."""
     import torch
     from src.pipeline import FeatureExtractor, create_window
     from src.synth import make_batch_device
-    G = 2 * torch.cuda.get_device_properties(0).multi_processor_count
+    G = grid()
     cap = G * 256
     B, n = cap + 9000, 1800
     x = make_batch_device(B, "cuda", base_seed=3, n_samples=n)
@@ -179,7 +188,7 @@ def test_many_near_ties():
     import torch
     from src.pipeline import FeatureExtractor, create_window
     from src.synth import make_batch
-    G = 2 * torch.cuda.get_device_properties(0).multi_processor_count
+    G = grid()
     B = 5 * G + 37
     base = make_batch(64, base_seed=900)
     tie = near_tie_clip()

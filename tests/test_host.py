@@ -84,6 +84,11 @@ def _riff(chunks):
     return b"RIFF" + len(body).to_bytes(4, "little") + body
 
 
+def _riff_size(blob, size):
+    """blob with its RIFF size field replaced (the wave module reads every chunk through it)"""
+    return blob[:4] + int(size).to_bytes(4, "little") + blob[8:]
+
+
 def _fmt(tag, ch, sr, bits):
     import struct
     return struct.pack("<HHLLHH", tag, ch, sr, sr * ch * ((bits + 7) // 8), ch * ((bits + 7) // 8), bits)
@@ -106,6 +111,11 @@ def test_riff_reader_equals_wave_module(tmp_path):
         "truncated": _riff([(b"fmt ", _fmt(1, 1, 44100, 16)), (b"data", pcm)])[:-500],
         "bits24": _riff([(b"fmt ", _fmt(1, 1, 44100, 24)), (b"data", pcm[:999])]),
         "not_riff": b"RIFX" + b"\0" * 40,
+        # RIFF size field 0 / ending inside the data / ending inside the fmt chunk / too large
+        "riff0": _riff_size(_riff([(b"fmt ", _fmt(1, 1, 44100, 16)), (b"data", pcm)]), 0),
+        "riff_short_data": _riff_size(_riff([(b"fmt ", _fmt(1, 1, 44100, 16)), (b"data", pcm)]), 4 + 24 + 8 + 1001),
+        "riff_short_fmt": _riff_size(_riff([(b"fmt ", _fmt(1, 1, 44100, 16)), (b"data", pcm)]), 4 + 8 + 10),
+        "riff_large": _riff_size(_riff([(b"fmt ", _fmt(1, 1, 44100, 16)), (b"data", pcm)]), 1 << 30),
     }
     for name, blob in cases.items():
         p = tmp_path / (name + ".wav")
@@ -146,6 +156,9 @@ def test_native_wav_reader_equals_python_reader(tmp_path):
         ("truncated", _riff([(b"fmt ", _fmt(1, 1, 44100, 16)), (b"data", pcm)])[:-500]),
         ("empty", _riff([(b"fmt ", _fmt(1, 1, 44100, 16)), (b"data", b"")])),
         ("not_riff", b"RIFX" + b"\0" * 40),
+        ("riff0", _riff_size(_riff([(b"fmt ", _fmt(1, 1, 44100, 16)), (b"data", pcm)]), 0)),
+        ("riff_short_data", _riff_size(_riff([(b"fmt ", _fmt(1, 1, 44100, 16)), (b"data", pcm)]), 4 + 24 + 8 + 1001)),
+        ("riff_large", _riff_size(_riff([(b"fmt ", _fmt(1, 1, 44100, 16)), (b"data", pcm)]), 1 << 30)),
     ]
     paths = []
     for name, blob in cases * 3:  # repeated: several threads, chunks of 8 files
@@ -157,7 +170,7 @@ def test_native_wav_reader_equals_python_reader(tmp_path):
     kind, ns, off = np.zeros(n, np.int32), np.zeros(n, np.int64), np.zeros(n, np.int64)
     from src.dataset import _cpaths
     assert L.dsp_wav_scan(_cpaths(paths), n, 4, kind.ctypes.data, ns.ctypes.data, off.ctypes.data) == 0
-    native = {"mono16": 1, "mono16_odd_bytes": 1, "mono8_odd_list": 2, "fmt18": 1, "empty": 1}
+    native = {"mono16": 1, "mono16_odd_bytes": 1, "mono8_odd_list": 2, "fmt18": 1, "empty": 1, "riff_large": 1}
     for p, k, m in zip(paths, kind, ns):
         name = p.rsplit("/", 1)[1].rsplit("_", 1)[0]
         assert k == native.get(name, 0), name

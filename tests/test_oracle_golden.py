@@ -86,3 +86,21 @@ def test_knn_oracle_self_query(knn_golden):
     idx, dist, _ = oracle.knn(X, g["ytr"][:800], X, 5, n_classes=10, self_offset=0)
     assert np.array_equal(idx, g["self5/idx"])
     assert np.array_equal(dist, g["self5/dist"])
+
+
+def test_np_reference_bit_exact(golden):
+    """oracle/np_reference.py (the reference's per-clip numpy loop, bench.py's
+    cpu_baseline_reference_semantics leg) reproduces the reference's golden outputs bit for bit."""
+    import np_reference
+    names = golden["clip_names"]
+    for key, L, S, wname, vad in golden_keys(golden):
+        window = golden["window/%s_%d" % (wname, L)]
+        for i in range(len(names)):
+            st, feat, s0, s1, nf = np_reference.process_clip(golden_clip(golden, i), L, S, window, do_vad=bool(vad))
+            assert st == golden[key + "/status"][i], (key, names[i])
+            if st:
+                continue
+            assert np.array_equal(feat, golden[key + "/feat"][i]), (key, names[i])
+            assert nf == golden[key + "/n_frames"][i], (key, names[i])
+            if vad:
+                assert (s0, s1) == tuple(golden[key + "/start_end"][i]), (key, names[i])
