@@ -479,13 +479,16 @@ __device__ __forceinline__ float lane_xor_f(float v, int m, int lane)
     const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
     return __int_as_float((lane & 32) ? r[0] : r[1]);
 }
-template <int NH, typename K>
+// NMAX < 64 (NH = 1): only the stages of a sort of NMAX-element groups -- each group of NMAX lanes
+// sorted on its own (keys past the real ones padded with the max key)
+template <int NH, typename K, int NMAX = 64 * NH>
 __device__ __forceinline__ void wave_bitonic(K (&a)[NH], int lane)
 {
+    static_assert(NMAX == 64 * NH || (NH == 1 && NMAX >= 2 && NMAX < 64 && (NMAX & (NMAX - 1)) == 0), "group size");
     // the lane index opaque here: the per-stage lane masks are then computed where they are used
     // instead of being hoisted out of a persistent loop and held (spilled) in SGPR pairs
     asm volatile("" : "+v"(lane));
-    constexpr int N = 64 * NH;
+    constexpr int N = NMAX;
 #pragma unroll
     for (int size = 2; size <= N; size <<= 1) {
 #pragma unroll

@@ -44,6 +44,10 @@
 #define DSP_ABL 0 // outputs are wrong): skip 1 = R4 frames, 2 = R5 jobs, 4 = R2 sign bits,
 #endif            // 8 = VAD pass-A partial moments -- the per-phase VALU budget of DESIGN.md §8
 
+#ifndef EXTRACT_STAGGER_US
+#define EXTRACT_STAGGER_US 0
+#endif
+
 namespace dsp {
 
 static constexpr int NT = EXTRACT_THREADS;
@@ -982,7 +986,12 @@ __device__ __forceinline__ void r5_fast(const Ctx &c, int F, float *featb, int w
         if (job < 3) {  // median by an in-wave bitonic sort
             unsigned a[2] = {in0 ? fkey(x0) : ~0u, in1 ? fkey(x1) : ~0u};
             float v0, v1;
-            if (F <= 64) {
+            if (F <= 32) {  // (the typical crop: 15 compare-exchange stages instead of 21)
+                unsigned b[1] = {a[0]};
+                wave_bitonic<1, unsigned, 32>(b, lane);
+                v0 = fkey_value(sorted_at<1>(b, r0));
+                v1 = fkey_value(sorted_at<1>(b, r1));
+            } else if (F <= 64) {
                 unsigned b[1] = {a[0]};
                 wave_bitonic<1>(b, lane);
                 v0 = fkey_value(sorted_at<1>(b, r0));
@@ -1807,6 +1816,13 @@ void extract_kernel(ExtractParams p)
     }
     build_window(p, c, tid, lane, wid);
     WG_CK(18);
+#if EXTRACT_STAGGER_US > 0  // A/B: the workgroups after the first G/3 start EXTRACT_STAGGER_US apart
+    if constexpr (FAST) {
+        const int slot = (int)blockIdx.x / max(1, (int)gridDim.x / EXTRACT_WG_PER_CU);
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), dt = 100ull * EXTRACT_STAGGER_US * slot;
+        while (__builtin_amdgcn_s_memrealtime() - t0 < dt) __builtin_amdgcn_s_sleep(8);
+    }
+#endif
     const ClipQueue Q = queue_open(p, sh);
     if (tid == 0) {
         sh->next = queue_next(Q, sh);

@@ -27,6 +27,7 @@ CLIP_FLAG_VAD_EXACT = 0x100
 ABI_VERSION = 6  # include/dsp_audiorec.h DSP_ABI_VERSION this binding is typed for
 QUEUE_WS_BYTES = 4096  # DSP_QUEUE_WS_BYTES
 OUT_ROW_WORDS = 19  # DSP_OUT_ROW_WORDS: feat[15] (f32), start, end, n_frames, status
+KNN_REF_READY = 1  # DSP_KNN_REF_READY
 
 EXPORTS = ("dsp_extract_lds_bytes", "dsp_extract_features", "dsp_extract_general_workspace_bytes",
            "dsp_extract_general", "dsp_knn_workspace_bytes", "dsp_knn_workspace_fallbacks_offset",
@@ -83,7 +84,7 @@ def load_library(path=LIB_PATH):
         L.dsp_knn_workspace_fallbacks_offset.restype = sz  # (older A/B variants lack it)
         L.dsp_knn_workspace_fallbacks_offset.argtypes = [i64, i64, i32, i32]
     L.dsp_knn_classify.restype = i32
-    L.dsp_knn_classify.argtypes = [vp, vp, i64, vp, i64, i32, i32, i64, i32, vp, vp, vp, vp, sz, vp]
+    L.dsp_knn_classify.argtypes = [vp, vp, i64, vp, i64, i32, i32, i64, i32, vp, vp, vp, vp, sz, i32, vp]
     L.dsp_zscore_fit.restype = i32
     L.dsp_zscore_fit.argtypes = [vp, i64, i32, vp, vp, vp]
     L.dsp_zscore_apply.restype = i32

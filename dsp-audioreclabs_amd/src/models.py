@@ -10,7 +10,7 @@ nothing.  The reference's MLP (models.py:77-221, PyTorch training) is out of sco
 """
 import numpy as np
 
-from .pipeline import knn_classify
+from .pipeline import KnnIndex
 
 
 class TraditionalClassifier:
@@ -45,24 +45,19 @@ class TraditionalClassifier:
         # classes_ sorted as in scikit-learn; the vote's smallest-index tie break is then the
         # smallest label (scipy.stats.mode)
         self.classes_, codes = np.unique(y, return_inverse=True)
-        import torch
-        from . import _hip
-        d = _hip.require_device()
-        self._X = torch.as_tensor(X, device=d)
-        self._codes = torch.as_tensor(codes.astype(np.int32), device=d)
+        # the reference set on the device, converted for the screen at the first query and kept
+        self._index = KnnIndex(X, codes.astype(np.int32), self.n_neighbors, n_classes=len(self.classes_))
         return self
 
     def kneighbors(self, X_test):
         """(distances, indices) [n, k] like KNeighborsClassifier.kneighbors(X_test)."""
-        idx, dist, _ = knn_classify(self._X, self._codes, np.asarray(X_test, dtype=np.float64), self.n_neighbors,
-                                    with_pred=False)
+        idx, dist, _ = self._index.query(np.asarray(X_test, dtype=np.float64))
         return dist.cpu().numpy(), idx.cpu().numpy().astype(np.int64)
 
     def predict(self, X_test):
         if self.classifier_type != 'knn':
             return self.model.predict(X_test)
-        _, _, pred = knn_classify(self._X, self._codes, np.asarray(X_test, dtype=np.float64), self.n_neighbors,
-                                  n_classes=len(self.classes_))
+        _, _, pred = self._index.query(np.asarray(X_test, dtype=np.float64))
         return self.classes_[pred.cpu().numpy()]
 
     def evaluate(self, X_test, y_test):

@@ -192,38 +192,61 @@ def process_audio_batch(pcm, offsets=None, frame_length=1102, frame_shift=441, w
     return dict(fx(pcm, offsets, max_len))
 
 
+class KnnIndex:
+    """A reference set prepared for ``dsp_knn_classify`` -- KNeighborsClassifier.fit's side
+    (src/models.py:52-55): the first query converts the rows for the screen into this index's
+    workspace, and every later query against the same set skips that step (DSP_KNN_REF_READY).
+    ``query`` is predict / kneighbors.  One query at a time per index (a workspace is a launch's
+    scratch); the workspace grows to the largest query batch seen."""
+
+    def __init__(self, ref, ref_labels, k, n_classes=None, with_pred=True):
+        import torch
+        self.device = _hip.require_device()
+        self.ref = _as_device(ref, torch.float64, self.device)
+        self.Nr, self.D = self.ref.shape
+        self.k = int(k)
+        self.labels = _as_device(ref_labels, torch.int32, self.device) if (ref_labels is not None and with_pred) else None
+        self.n_classes = int(n_classes or 0)
+        self._ws, self._ready = None, False
+
+    def query(self, query, self_offset=-1, stats=None):
+        """(idx int32 [Nq,k], dist float64 [Nq,k], pred int32 [Nq] or None); a dict passed as
+        ``stats`` receives "fallbacks" (queries answered by the exhaustive fp64 scan; one host sync)."""
+        import torch
+        d, k = self.device, self.k
+        q = _as_device(query, torch.float64, d)
+        Nq = q.shape[0]
+        ws_bytes = _hip.lib().dsp_knn_workspace_bytes(self.Nr, Nq, self.D, k)
+        if ws_bytes == 0 and Nq > 0:
+            raise ValueError("unsupported KNN shape (1 <= D <= 4096, 1 <= k <= 32)")
+        if self._ws is None or self._ws.numel() < ws_bytes:
+            self._ws, self._ready = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=d), False
+        idx = torch.empty((Nq, k), dtype=torch.int32, device=d)
+        dist = torch.empty((Nq, k), dtype=torch.float64, device=d)
+        pred = torch.empty(Nq, dtype=torch.int32, device=d) if self.labels is not None else None
+        flags = _hip.KNN_REF_READY if self._ready else 0
+        rc = _hip.lib().dsp_knn_classify(_hip.ptr(self.ref), _hip.ptr(self.labels), self.Nr, _hip.ptr(q), Nq,
+                                         self.D, k, int(self_offset), self.n_classes, _hip.ptr(idx),
+                                         _hip.ptr(dist), _hip.ptr(pred), _hip.ptr(self._ws), self._ws.numel(),
+                                         flags, _hip.stream_handle(d))
+        _hip.check(rc, "dsp_knn_classify")
+        self._ready = self._ready or (Nq > 0 and self.Nr > 0)
+        if stats is not None and Nq > 0:
+            off = _hip.lib().dsp_knn_workspace_fallbacks_offset(self.Nr, Nq, self.D, k)
+            stats["fallbacks"] = int(self._ws[off:off + 4].view(torch.int32).item())
+        return idx, dist, pred
+
+
 def knn_classify(ref, ref_labels, query, k, self_offset=-1, n_classes=None, with_pred=True, stats=None):
-    """Exact k-NN (KNeighborsClassifier semantics) on the device.
+    """Exact k-NN (KNeighborsClassifier semantics) on the device, one-shot (``KnnIndex`` keeps the
+    prepared reference set across queries).
 
     ref [Nr, D] / query [Nq, D] float64 (cast if needed), ref_labels int [Nr].
     Returns (idx int32 [Nq,k], dist float64 [Nq,k], pred int32 [Nq] or None).  A dict passed as
     ``stats`` receives "fallbacks": the queries answered by the exhaustive fp64 fallback (one host
     sync).
     """
-    import torch
-    d = _hip.require_device()
-    ref = _as_device(ref, torch.float64, d)
-    q = _as_device(query, torch.float64, d)
-    Nr, D = ref.shape
-    Nq = q.shape[0]
-    lbl = _as_device(ref_labels, torch.int32, d) if (ref_labels is not None and with_pred) else None
-    if n_classes is None:
-        n_classes = 0
-    ws_bytes = _hip.lib().dsp_knn_workspace_bytes(Nr, Nq, D, k)
-    if ws_bytes == 0 and Nq > 0:
-        raise ValueError("unsupported KNN shape (1 <= D <= 4096, 1 <= k <= 32)")
-    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=d)
-    idx = torch.empty((Nq, k), dtype=torch.int32, device=d)
-    dist = torch.empty((Nq, k), dtype=torch.float64, device=d)
-    pred = torch.empty(Nq, dtype=torch.int32, device=d) if lbl is not None else None
-    rc = _hip.lib().dsp_knn_classify(_hip.ptr(ref), _hip.ptr(lbl), Nr, _hip.ptr(q), Nq, D, k,
-                                     int(self_offset), int(n_classes), _hip.ptr(idx), _hip.ptr(dist),
-                                     _hip.ptr(pred), _hip.ptr(ws), ws_bytes, _hip.stream_handle(d))
-    _hip.check(rc, "dsp_knn_classify")
-    if stats is not None and Nq > 0:
-        off = _hip.lib().dsp_knn_workspace_fallbacks_offset(Nr, Nq, D, k)
-        stats["fallbacks"] = int(ws[off:off + 4].view(torch.int32).item())
-    return idx, dist, pred
+    return KnnIndex(ref, ref_labels, k, n_classes, with_pred).query(query, self_offset, stats)
 
 
 def zscore_fit(X):

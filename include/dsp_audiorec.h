@@ -34,7 +34,8 @@ extern "C" {
                               3: queue_ws is 64 bytes (per-XCD chunk counters);
                               4: the batch WAV reader (dsp_wav_scan / dsp_wav_read);
                               5: queue_ws is 4 KiB (each counter on its own 256-B line);
-                              6: the extraction entry points take out_stride (packed result rows) */
+                              6: the extraction entry points take out_stride (packed result rows);
+                                 dsp_knn_classify takes flags (DSP_KNN_REF_READY) */
 
 /* return codes */
 #define DSP_OK 0
@@ -169,17 +170,22 @@ int dsp_extract_general(const void *pcm, int sample_bytes, const int64_t *offset
  *              neighbour list (kneighbors(X=None) semantics); -1: no exclusion.
  * idx        int32 [Nq, k] (-1 where fewer than k candidates), dist float64 [Nq, k],
  * pred       int32 [Nq] (may be NULL, or ref_labels NULL, to skip the vote)
- * workspace  device scratch of dsp_knn_workspace_bytes(Nr, Nq, D, k) bytes.
+ * workspace  device scratch of dsp_knn_workspace_bytes(Nr, Nq, D, k) bytes.  Its first part holds
+ *            the reference set converted for the screen, at offsets that depend on (Nr, D) only.
+ * flags      DSP_KNN_REF_READY: the workspace already holds that conversion, left by an earlier call
+ *            with the same ref, Nr, D and k on the same stream (any Nq): the conversion -- the
+ *            fit() side of KNeighborsClassifier, src/models.py:52-55 -- is skipped.  0: convert.
  * Requires 1 <= D <= 4096, 1 <= k <= 32.  D <= 32: queries in registers, reference tiles in LDS;
  * D > 32 (the sequence method's flattened features): dimensions walked in chunks of 16.
  */
+#define DSP_KNN_REF_READY 1
 size_t dsp_knn_workspace_bytes(int64_t Nr, int64_t Nq, int D, int k);
 /* Diagnostic: byte offset in that workspace of an int32 that dsp_knn_classify leaves holding the
  * number of queries the screen could not certify (answered by the exhaustive fp64 fallback). */
 size_t dsp_knn_workspace_fallbacks_offset(int64_t Nr, int64_t Nq, int D, int k);
 int dsp_knn_classify(const double *ref, const int32_t *ref_labels, int64_t Nr, const double *query,
                      int64_t Nq, int D, int k, int64_t self_offset, int n_classes, int32_t *idx,
-                     double *dist, int32_t *pred, void *workspace, size_t workspace_bytes,
+                     double *dist, int32_t *pred, void *workspace, size_t workspace_bytes, int flags,
                      void *stream);
 
 /*

@@ -73,9 +73,9 @@ def test_host_argument_checks(lib):
     assert lib.dsp_knn_workspace_bytes(100, 100, 15, 33) == 0
     assert lib.dsp_knn_workspace_bytes(100, 100, 15, 5) > 0
     k = lib.dsp_knn_classify
-    assert k(p, p, 100, p, 10, 0, 3, -1, 0, p, p, p, p, 1 << 20, None) == _hip.DSP_ERR_ARGS
-    assert k(p, p, 100, p, 10, 15, 3, -1, 0, p, p, p, None, 0, None) == _hip.DSP_ERR_WORKSPACE
-    assert k(p, p, 100, p, 0, 15, 3, -1, 0, None, None, None, None, 0, None) == _hip.DSP_OK
+    assert k(p, p, 100, p, 10, 0, 3, -1, 0, p, p, p, p, 1 << 20, 0, None) == _hip.DSP_ERR_ARGS
+    assert k(p, p, 100, p, 10, 15, 3, -1, 0, p, p, p, None, 0, 0, None) == _hip.DSP_ERR_WORKSPACE
+    assert k(p, p, 100, p, 0, 15, 3, -1, 0, None, None, None, None, 0, 0, None) == _hip.DSP_OK
     assert lib.dsp_zscore_fit(None, 10, 15, p, p, None) == _hip.DSP_ERR_ARGS
     g = lib.dsp_extract_general
     gargs = lambda sb=2, ws=None, nws=0, n=4: (p, sb, p, None, n, 0, 44100, 1102, 441, p, 1, 0.5, 0.1, 1.5,

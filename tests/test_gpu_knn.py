@@ -283,3 +283,26 @@ def test_knn_on_extracted_features_20k():
     assert np.array_equal(dist.cpu().numpy()[lo:lo + 2000], d0), st
     assert np.array_equal(pred.cpu().numpy()[lo:lo + 2000], p0), st
     print("extracted-feature KNN: %d of %d queries fell back to the exhaustive fp64 scan" % (st["fallbacks"], n))
+
+
+def test_knn_index_prepared_queries_equal_one_shot():
+    """KnnIndex (fit once, query many: DSP_KNN_REF_READY skips the reference set's conversion on
+    every query after the first) gives exactly the one-shot knn_classify answers, for query
+    batches of different sizes (the workspace grows and is re-prepared) and for self-queries."""
+    import torch
+    from src.pipeline import KnnIndex, knn_classify
+    rng = np.random.default_rng(12)
+    n, d, k = 40000, 15, 5
+    X = rng.standard_normal((n, d))
+    y = rng.integers(0, 10, n).astype(np.int32)
+    Xd, yd = torch.as_tensor(X, device="cuda"), torch.as_tensor(y, device="cuda")
+    index = KnnIndex(Xd, yd, k, n_classes=10)
+    for lo, hi in [(0, 500), (500, 9000), (9000, 9100), (20000, 40000), (0, 500)]:
+        got = index.query(Xd[lo:hi], self_offset=lo)
+        want = knn_classify(Xd, yd, Xd[lo:hi], k, self_offset=lo, n_classes=10)
+        for g, w in zip(got, want):
+            assert torch.equal(g, w), (lo, hi)
+    i0, d0, p0 = oracle.knn(X, y, X[20000:20300], k, n_classes=10, self_offset=20000)
+    i1, d1, p1 = index.query(Xd[20000:20300], self_offset=20000)
+    assert np.array_equal(i1.cpu().numpy(), i0) and np.array_equal(d1.cpu().numpy(), d0)
+    assert np.array_equal(p1.cpu().numpy(), p0)

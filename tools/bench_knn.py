@@ -37,28 +37,43 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--cpu-queries", type=int, default=200)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--data", choices=("extracted", "synthetic"), default="extracted",
+                    help="extracted: the z-scored 15-d features of --ref synthetic utterances (BASELINE "
+                         "configs[4]); synthetic: Gaussian vectors around 10 class centres (rounds 1-5)")
     a = ap.parse_args()
     import torch
-    from src.pipeline import knn_classify
+    from src.pipeline import FeatureExtractor, KnnIndex, zscore_apply, zscore_fit
 
-    rng = np.random.default_rng(0)
-    centres = rng.standard_normal((10, a.dim)) * 1.5
-    y = rng.integers(0, 10, a.ref).astype(np.int32)
-    X = centres[y] + rng.standard_normal((a.ref, a.dim))
-    X = (X - X.mean(0)) / X.std(0)
-    q0 = 0
     dev = torch.device("cuda", 0)
-    Xd = torch.as_tensor(X, device=dev)
-    yd = torch.as_tensor(y, device=dev)
+    if a.data == "extracted":
+        from src.synth import make_batch_device
+        a.dim = 15
+        out = FeatureExtractor(1102, 441, "hamming", True, device=dev)(make_batch_device(a.ref, dev, base_seed=0))
+        assert not (out["status"] & 0xFF).any().item()
+        feat = out["feat"].to(torch.float64)
+        mu, sd = zscore_fit(feat)
+        Xd = zscore_apply(feat, mu, sd)
+        yd = (torch.arange(a.ref, device=dev) % 10).to(torch.int32)
+        X, y = Xd.cpu().numpy(), yd.cpu().numpy()
+    else:
+        rng = np.random.default_rng(0)
+        centres = rng.standard_normal((10, a.dim)) * 1.5
+        y = rng.integers(0, 10, a.ref).astype(np.int32)
+        X = centres[y] + rng.standard_normal((a.ref, a.dim))
+        X = (X - X.mean(0)) / X.std(0)
+        Xd = torch.as_tensor(X, device=dev)
+        yd = torch.as_tensor(y, device=dev)
+    q0 = 0
     Qd = Xd[q0:q0 + a.queries]
-    knn_classify(Xd, yd, Qd, a.k, self_offset=q0)  # warm-up (workspace, code objects)
+    index = KnnIndex(Xd, yd, a.k, n_classes=10)
+    index.query(Qd, self_offset=q0)  # fit (the reference set converted) + warm-up (code objects)
     torch.cuda.synchronize()
     times = []
     for _ in range(a.reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         st = {}
-        idx, dist, pred = knn_classify(Xd, yd, Qd, a.k, self_offset=q0, stats=st)
+        idx, dist, pred = index.query(Qd, self_offset=q0, stats=st)
         e1.record()
         torch.cuda.synchronize()
         times.append(e0.elapsed_time(e1) / 1e3)
@@ -68,7 +83,11 @@ def main():
            "value": round(pairs / t, 1), "unit": "pairs/s", "ms": round(t * 1e3, 4),
            "fallbacks": st.get("fallbacks"),
            "config": {"ref": a.ref, "queries": a.queries, "dim": a.dim, "k": a.k, "self_query": True,
-                      "data": "synthetic z-scored 15-d vectors around 10 class centres"},
+                      "data": ("z-scored 15-d features of %d synthetic utterances (fused extraction + "
+                               "normalize_features on the device), labels i mod 10" % a.ref)
+                      if a.data == "extracted" else "synthetic z-scored 15-d vectors around 10 class centres",
+                      "timed": "queries against the prepared reference set (KnnIndex: the fp32 conversion "
+                               "is the fit, done once)"},
            "roofline": {"bound": "mfma-f32", "achieved": round(pairs * FLOP_PER_PAIR / t / 1e12, 2),
                         "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
                         "frac": round(pairs * FLOP_PER_PAIR / t / 1e12 / VALU_PEAK_TFS, 4),
