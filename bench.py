@@ -119,7 +119,7 @@ def timed_launches(fn, n, stream):
 
 
 def assemble_result(args, world, ranks_seen, rehearsal, backend_name, C, total_frames, elapsed_x, elapsed_g,
-                    kern_ms):
+                    kern_ms, kern_ms_iso=None):
     """The bench line (rank 0).  world > 1: ``value`` is the K steps of extraction + all-gather
     (configs[3] as BASELINE defines it); ``value_extract_only`` the same steps without the exchange."""
     N = 44100
@@ -130,6 +130,9 @@ def assemble_result(args, world, ranks_seen, rehearsal, backend_name, C, total_f
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
             "kernel": "dsp::extract_kernel", "kernel_avg_ms": round(kern_ms, 5),
+            "kernel_avg_source": "HIP events on the launch stream around the %d timed steps, / %d (per step: "
+                                 "extract_kernel + extract_exact_kernel's early exit + launch gap)" % (args.steps, args.steps),
+            "kernel_avg_ms_isolated_launches": None if kern_ms_iso is None else round(kern_ms_iso, 5),
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "per_unit": "2*44100 B in + 76 B out per clip"}
     pmc = os.path.join(REPO, "profiles", "pmc_extract.json")
@@ -248,8 +251,10 @@ def main():
     torch.cuda.synchronize(dev)
 
     K = args.steps
-    # per-launch kernel time on the launch stream (HIP events), for the roofline
-    kern_ms = timed_launches(lambda: fx(pool[0]), max(3, min(K, 10)), stream) if P == 1 else \
+    # isolated launches, each bracketed by HIP events: reported beside the timed region's figure;
+    # after the host-side syncs above the GPU has idled and its clock ramps back up over the first
+    # few launches (round 6 kernel trace: 2.75 -> 2.45 ms), so these read high
+    kern_ms_iso = timed_launches(lambda: fx(pool[0]), max(3, min(K, 10)), stream) if P == 1 else \
         float(np.mean([timed_launches(lambda: fx(pool[p]), 2, stream) for p in range(P)]))
     # the timed steps: captured once into a HIP graph and replayed, so host overhead (ctypes,
     # Python) does not throttle short launches; --no-graph launches each step from Python
@@ -268,16 +273,22 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(stream)
     if graph is not None:
         graph.replay()
     else:
         for i in range(K):
             fx(pool[i % P])
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed_x = time.perf_counter() - t0  # extraction only
+    # the roofline's per-launch time: HIP events on the launch stream around the K timed steps, / K
+    # (each step = extract_kernel + extract_exact_kernel's early exit + the gap between launches)
+    kern_ms = ev0.elapsed_time(ev1) / K
     my_frames = float(sum(frames[i % P] for i in range(K)))
     # the timed steps checked: the last replayed step's outputs (still in the extractor's buffers)
     # against one eager launch of the same batch into fresh buffers, bit for bit
@@ -323,12 +334,13 @@ def main():
               "what": "every clip's packed 76-B result row (feat, start/end, n_frames, status) as written by "
                       "the kernel, one %s all_gather_into_tensor, no pack/unpack kernels" % backend_name}
     if world > 1:
-        t = torch.tensor([elapsed_x, elapsed_g, my_frames, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed_x, elapsed_g, my_frames, kern_ms, kern_ms_iso], dtype=torch.float64, device=dev)
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t.clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         elapsed_x, elapsed_g, total_frames, kern_ms = tmax[0].item(), tmax[1].item(), tsum[2].item(), tmax[3].item()
+        kern_ms_iso = tmax[4].item()
         if timed_ok is not None:  # every rank's last timed step
             ok = torch.tensor([1 if timed_ok else 0], dtype=torch.int32, device=dev)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
@@ -345,7 +357,7 @@ def main():
     result = None
     if rank == 0:
         result = assemble_result(args, world, ranks_seen, rehearsal, backend_name, C, total_frames, elapsed_x,
-                                 elapsed_g, kern_ms)
+                                 elapsed_g, kern_ms, kern_ms_iso)
         if peaks is not None:
             r = result["roofline"]
             r["measured_read_peak_gbs"] = peaks["read_gbs"]

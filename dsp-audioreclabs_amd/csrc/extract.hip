@@ -44,10 +44,6 @@
 #define DSP_ABL 0 // outputs are wrong): skip 1 = R4 frames, 2 = R5 jobs, 4 = R2 sign bits,
 #endif            // 8 = VAD pass-A partial moments -- the per-phase VALU budget of DESIGN.md §8
 
-#ifndef EXTRACT_STAGGER_US
-#define EXTRACT_STAGGER_US 0
-#endif
-
 namespace dsp {
 
 static constexpr int NT = EXTRACT_THREADS;
@@ -1816,13 +1812,9 @@ void extract_kernel(ExtractParams p)
     }
     build_window(p, c, tid, lane, wid);
     WG_CK(18);
-#if EXTRACT_STAGGER_US > 0  // A/B: the workgroups after the first G/3 start EXTRACT_STAGGER_US apart
-    if constexpr (FAST) {
-        const int slot = (int)blockIdx.x / max(1, (int)gridDim.x / EXTRACT_WG_PER_CU);
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), dt = 100ull * EXTRACT_STAGGER_US * slot;
-        while (__builtin_amdgcn_s_memrealtime() - t0 < dt) __builtin_amdgcn_s_sleep(8);
-    }
-#endif
+    // (starting the second and third workgroup of each CU 2 or 5 us after the first, against the
+    // lockstep start of round 5's stamps: 12.5k clips 0.405-0.415 against 0.400-0.403 ms per step,
+    // 100k unchanged -- profiles/r06d_ab_stagger.txt; not kept)
     const ClipQueue Q = queue_open(p, sh);
     if (tid == 0) {
         sh->next = queue_next(Q, sh);

@@ -585,6 +585,47 @@ __device__ __forceinline__ double rdist64(const double *__restrict__ a, const do
     }
     return d;
 }
+// The same for D <= 16 (the 15-d features) with the query in registers and the reference row's
+// loads all issued before its first use: the rolled loop above waited for each of its loads in
+// turn, so a re-rank or a fallback scan paid ~D memory latencies per row (round 6: the 3
+// fallback queries of the 100k x 100k self-query on extracted features took 1.06 ms).
+struct QRow16 {
+    double v[16];
+};
+__device__ __forceinline__ QRow16 qrow16(const double *__restrict__ qx, int D)
+{
+    QRow16 q;
+#pragma unroll
+    for (int c = 0; c < 16; c++) q.v[c] = c < D ? qx[c] : 0.0;
+    return q;
+}
+__device__ __forceinline__ void row16_load(double (&b)[16], const double *__restrict__ r, int D)
+{
+#pragma unroll
+    for (int c = 0; c < 16; c++) b[c] = c < D ? r[c] : 0.0;
+}
+__device__ __forceinline__ double rdist64_16(const QRow16 &q, const double (&b)[16], int D)
+{
+    double d = 0.0;
+#pragma unroll
+    for (int c = 0; c < 16; c++)
+        if (c < D) {
+            const double t = q.v[c] - b[c];
+            d = d + t * t;
+        }
+    return d;
+}
+// rdist64 through the register path when D <= 16
+__device__ __forceinline__ double rdist64_q(const QRow16 &q, const double *__restrict__ qx, const double *__restrict__ r,
+                                            int D)
+{
+    if (D <= 16) {
+        double b[16];
+        row16_load(b, r, D);
+        return rdist64_16(q, b, D);
+    }
+    return rdist64(qx, r, D);
+}
 #pragma clang fp contract(on)
 
 __device__ __forceinline__ bool cand_less(double da, int ia, double db, int ib)
@@ -674,6 +715,7 @@ __global__ __launch_bounds__(64) void knn_merge1(const double *__restrict__ ref,
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= Nq) return;
     const double *qx = query + q * D;
+    const QRow16 q16 = qrow16(qx, D <= 16 ? D : 0);
     double dl[KM];
     int il[KM];
 #pragma unroll
@@ -682,7 +724,13 @@ __global__ __launch_bounds__(64) void knn_merge1(const double *__restrict__ ref,
         il[i] = 0x7fffffff;
     }
     double qn = 0.0;
-    for (int c = 0; c < D; c++) qn += qx[c] * qx[c];
+    if (D <= 16) {
+#pragma unroll
+        for (int c = 0; c < 16; c++)
+            if (c < D) qn += q16.v[c] * q16.v[c];
+    } else {
+        for (int c = 0; c < D; c++) qn += qx[c] * qx[c];
+    }
     // |fp32 screened distance - fp64 distance| <= err(d): fp32 rounding of the inputs and of the
     // sum (direct or expanded form), coefficients from the host (knn_err_coeffs)
     const double rmax = (double)__uint_as_float(*maxnorm_bits);
@@ -737,7 +785,7 @@ __global__ __launch_bounds__(64) void knn_merge1(const double *__restrict__ ref,
         for (int i = 0; i < KC; i++) {
             const double d = (double)dd[i];
             if (rr[i] < 0 || rr[i] == self || d - err(d) > keep) continue;
-            topk_fixed_insert<KM>(dl, il, rdist64(qx, ref + (int64_t)rr[i] * D, D), rr[i]);
+            topk_fixed_insert<KM>(dl, il, rdist64_q(q16, qx, ref + (int64_t)rr[i] * D, D), rr[i]);
         }
     }
     // certification: any row that was screened out has fp32 distance >= cut; its true fp64
@@ -855,6 +903,7 @@ __global__ __launch_bounds__(64) void knn_merge(const double *__restrict__ ref, 
     const bool live = qr < Nq;  // every lane takes part in the shuffles
     const int64_t q = live ? qr : Nq - 1;
     const double *qx = query + q * D;
+    const QRow16 q16 = qrow16(qx, D <= 16 ? D : 0);
     double dl[KM];
     int il[KM];
 #pragma unroll
@@ -863,7 +912,13 @@ __global__ __launch_bounds__(64) void knn_merge(const double *__restrict__ ref, 
         il[i] = 0x7fffffff;
     }
     double qn = 0.0;
-    for (int c = 0; c < D; c++) qn += qx[c] * qx[c];
+    if (D <= 16) {
+#pragma unroll
+        for (int c = 0; c < 16; c++)
+            if (c < D) qn += q16.v[c] * q16.v[c];
+    } else {
+        for (int c = 0; c < D; c++) qn += qx[c] * qx[c];
+    }
     // |fp32 screened distance - fp64 distance| <= err(d): fp32 rounding of the inputs and of the
     // sum (direct or expanded form), coefficients from the host (knn_err_coeffs)
     const double rmax = (double)__uint_as_float(*maxnorm_bits);
@@ -925,7 +980,7 @@ __global__ __launch_bounds__(64) void knn_merge(const double *__restrict__ ref, 
         for (int i = 0; i < KC; i++) {
             const double d = (double)dd[i];
             if (rr[i] < 0 || rr[i] == self || d - err(d) > keep) continue;
-            topk_fixed_insert<KM>(dl, il, rdist64(qx, ref + (int64_t)rr[i] * D, D), rr[i]);
+            topk_fixed_insert<KM>(dl, il, rdist64_q(q16, qx, ref + (int64_t)rr[i] * D, D), rr[i]);
         }
     }
 #pragma unroll
@@ -994,9 +1049,27 @@ __global__ __launch_bounds__(FB_T) void knn_fallback(const double *__restrict__ 
             dl[i] = INFINITY;
             il[i] = 0x7fffffff;
         }
-        for (int64_t r = tid; r < Nr; r += FB_T) {
-            if (self_offset >= 0 && r == self_offset + q) continue;
-            topk64_insert<KMAX>(dl, il, k, rdist64(qx, ref + r * D, D), (int)r);
+        if (D <= 16) {  // four rows in flight per thread, the query in registers
+            const QRow16 q16 = qrow16(qx, D);
+            for (int64_t r0 = tid; r0 < Nr; r0 += 4 * FB_T) {
+                double b[4][16];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int64_t r = r0 + (int64_t)u * FB_T;
+                    row16_load(b[u], ref + (r < Nr ? r : 0) * D, D);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int64_t r = r0 + (int64_t)u * FB_T;
+                    if (r < Nr && !(self_offset >= 0 && r == self_offset + q))
+                        topk64_insert<KMAX>(dl, il, k, rdist64_16(q16, b[u], D), (int)r);
+                }
+            }
+        } else {
+            for (int64_t r = tid; r < Nr; r += FB_T) {
+                if (self_offset >= 0 && r == self_offset + q) continue;
+                topk64_insert<KMAX>(dl, il, k, rdist64(qx, ref + r * D, D), (int)r);
+            }
         }
         // pairwise tree merge of the per-thread lists through LDS
         for (int width = FB_T; width > 1; width >>= 1) {
@@ -1028,21 +1101,32 @@ __global__ __launch_bounds__(FB_T) void knn_fallback(const double *__restrict__ 
 
 // ---- z-score (src/feature_extraction.py:157-181), numpy axis-0 order ---------------------
 #pragma clang fp contract(off)
-__global__ void zscore_fit_kernel(const double *X, int64_t N, int D, double *mean, double *std)
+// One wave per column: the rows are loaded 64 at a time (one per lane, all in flight together) and
+// added to the running sum in row order from the registers (wave-uniform, lane_read): numpy's
+// sequential axis-0 order exactly, without a dependent global load per row (round 5's one thread
+// per column: 46 ms for 100 000 x 15; the add chain itself is the floor).
+__global__ __launch_bounds__(64) void zscore_fit_kernel(const double *X, int64_t N, int D, double *mean, double *std)
 {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= D) return;
+    const int c = blockIdx.x, lane = threadIdx.x;
     double s = 0.0;
-    for (int64_t i = 0; i < N; i++) s = s + X[i * D + c];
+    for (int64_t b = 0; b < N; b += 64) {
+        const double x = b + lane < N ? X[(b + lane) * D + c] : 0.0;
+        const int cnt = (int)min((int64_t)64, N - b);
+        for (int j = 0; j < cnt; j++) s = s + lane_read(x, j);
+    }
     const double m = s / (double)N;
     double v = 0.0;
-    for (int64_t i = 0; i < N; i++) {
-        const double t = X[i * D + c] - m;
-        v = v + t * t;
+    for (int64_t b = 0; b < N; b += 64) {
+        const double x = b + lane < N ? X[(b + lane) * D + c] - m : 0.0;
+        const double t2 = x * x;
+        const int cnt = (int)min((int64_t)64, N - b);
+        for (int j = 0; j < cnt; j++) v = v + lane_read(t2, j);
     }
-    const double sd = sqrt(v / (double)N);
-    mean[c] = m;
-    std[c] = sd == 0.0 ? 1.0 : sd;
+    if (lane == 0) {
+        const double sd = sqrt(v / (double)N);
+        mean[c] = m;
+        std[c] = sd == 0.0 ? 1.0 : sd;
+    }
 }
 
 __global__ void zscore_apply_kernel(const double *X, int64_t N, int D, const double *mean,
@@ -1458,8 +1542,8 @@ extern "C" int dsp_zscore_fit(const double *X, int64_t N, int D, double *mean, d
                               void *stream)
 {
     if (!X || !mean || !std || N < 1 || D < 1) return DSP_ERR_ARGS;
-    hipLaunchKernelGGL(dsp::zscore_fit_kernel, dim3((D + 63) / 64), dim3(64), 0,
-                       (hipStream_t)stream, X, N, D, mean, std);
+    hipLaunchKernelGGL(dsp::zscore_fit_kernel, dim3((unsigned)D), dim3(64), 0, (hipStream_t)stream, X, N, D, mean,
+                       std);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? DSP_OK : DSP_ERR_HIP + (int)e;
 }

@@ -1,7 +1,8 @@
 """The multi-rank path with the HIP kernels in it: two processes on the one GPU of
 the box, joined by gloo (RCCL needs one GPU per rank), each extracting its shard_range block with
 the fused kernel and answering its block of KNN queries on the device, the results exchanged by
-src/distributed.py's packed all-gather exactly as bench.py does over RCCL.  The gathered results
+src/distributed.py's gather_rows (ONE all_gather_into_tensor of the kernel's packed 76-B result
+rows; 3 001 clips = 1 501 + 1 500, so the ragged-block path) exactly as bench.py does over RCCL.  The gathered results
 must equal one single-process launch bit for bit (features are position independent, so an odd
 shard size changes nothing) and the oracle's KNN."""
 import os
@@ -31,7 +32,7 @@ def _worker(rank, ws, port, out_dir):
     sys.path.insert(0, PKG)
     import torch.distributed as dist
     from src import distributed as D
-    from src.pipeline import FeatureExtractor, knn_classify
+    from src.pipeline import FeatureExtractor, KnnIndex
     from src.synth import make_batch
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -43,14 +44,12 @@ def _worker(rank, ws, port, out_dir):
         def make_shard(lo, hi):
             return torch.as_tensor(make_batch(hi - lo, base_seed=21, start=lo)).to(dev)
 
-        def extract(pcm):
-            out = fx(pcm)
-            return {k: out[k] for k in ("feat", "start_end", "n_frames", "status")}
-
-        got = D.extract_sharded(extract, make_shard, B)
+        got = D.extract_sharded(fx, make_shard, B)  # FeatureExtractor's rows -> gather_rows
+        assert got["rows"].shape == (B, 19)
         X = got["feat"].to(torch.float64)
         y = torch.arange(B, dtype=torch.int32, device=dev) % 4
-        idx, dist_, pred = D.knn_sharded(lambda r, lab, q, k, so: knn_classify(r, lab, q, k, self_offset=so),
+        index = KnnIndex(X, y, K, n_classes=4)  # fit once on every rank, query the rank's block
+        idx, dist_, pred = D.knn_sharded(lambda r, lab, q, k, so: index.query(q, self_offset=so),
                                          X, y, X, K, self_query=True)
         torch.cuda.synchronize(dev)
         if rank == 0:

@@ -6,6 +6,9 @@
 R=${GRAFT_REPO_ROOT:-$(pwd)}; T=${1:-r06f}; O=$R/gpurun_out/$T; mkdir -p $O; cd $R
 export TMPDIR=/tmp
 S=${STEPS:-tests prof pmc rehearsal knn}
+if [[ " $S " == *" counters "* ]]; then  # which memory-side counters this gfx950 exposes (MALL / DRAM)
+  (cd /tmp && timeout -k 10 120 rocprofv3 -L > $O/counters_all.txt 2>&1); grep -i -E "mall|dram|EA0_RD|EA_RD|tcc_ea" $O/counters_all.txt | head -60 > $O/counters_mem.txt; wc -l $O/counters_mem.txt
+fi
 if [[ " $S " == *" tests "* ]]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
   rc=$?; tail -2 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
