@@ -18,7 +18,8 @@
 //                       FMA -- sklearn euclidean_rdist), keeps the k best by (distance, index), and
 //                       certifies that no screened-out row can beat the k-th; otherwise the query
 //                       goes on a fallback list.
-//   4. knn_fallback     one workgroup per listed query: exhaustive fp64 scan.
+//   4. knn_fallback     exhaustive fp64 scan of the listed queries: each query's rows in parts,
+//                       one wave per part, the parts' lists merged by the last wave done.
 //   5. vote             majority label, smallest label on ties (scipy.stats.mode).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -932,15 +933,15 @@ __global__ __launch_bounds__(64) void knn_merge(const double *__restrict__ ref, 
     // cut: every row the screen did not keep has a screened distance >= cut (a seeded screen keeps
     // only rows below min(seed, the lists' thresholds))
     float kth = INFINITY, cut = seed ? seed[q] : INFINITY;
-    for (int s = j; s < nsplit; s += MG) {
+    auto load_split = [&](int s, int (&rr)[KC], float (&dd)[KC]) {
         const size_t o = ((size_t)s * Nq + q) * KC;
-        int rr[KC];
-        float dd[KC];
 #pragma unroll
         for (int i = 0; i < KC; i++) {
             rr[i] = cand_i[o + i];
             dd[i] = cand_d[o + i];
         }
+    };
+    auto pass1 = [&](const int (&rr)[KC], const float (&dd)[KC]) {
 #pragma unroll
         for (int i = 0; i < KC; i++) {
             // a value at or past this lane's k-th is not among the group's k smallest either
@@ -955,6 +956,25 @@ __global__ __launch_bounds__(64) void knn_merge(const double *__restrict__ ref, 
             kth = kth_of<KM>(k32, k);
         }
         if (rr[KC - 1] >= 0) cut = fminf(cut, dd[KC - 1]);
+    };
+    // short lists (KC <= 8): a lane's first two splits are loaded together and kept in registers
+    // for pass 2 (12 500 queries take 13 splits, 100 000 take 6: every split of MG = 8 lanes)
+    constexpr bool CACHE2 = KC <= 8;
+    constexpr int NC = CACHE2 ? KC : 1;
+    int rc0[NC], rc1[NC];
+    float dc0[NC], dc1[NC];
+    const bool h0 = CACHE2 && j < nsplit, h1 = CACHE2 && j + MG < nsplit;
+    if constexpr (CACHE2) {
+        if (h0) load_split(j, rc0, dc0);
+        if (h1) load_split(j + MG, rc1, dc1);
+        if (h0) pass1(rc0, dc0);
+        if (h1) pass1(rc1, dc1);
+    }
+    for (int s = j + (CACHE2 ? 2 * MG : 0); s < nsplit; s += MG) {
+        int rr[KC];
+        float dd[KC];
+        load_split(s, rr, dd);
+        pass1(rr, dd);
     }
 #pragma unroll
     for (int m = 1; m < MG; m <<= 1) {
@@ -967,20 +987,49 @@ __global__ __launch_bounds__(64) void knn_merge(const double *__restrict__ ref, 
     // candidates at or below t32
     const double t32 = (double)kth;
     const double keep = t32 < INFINITY ? t32 + err(t32) : INFINITY;
-    for (int s = j; s < nsplit; s += MG) {
-        const size_t o = ((size_t)s * Nq + q) * KC;
+    // the candidates that pass are few (about k per query over its MG lanes): a bit mask, then ONE
+    // rolled loop that picks each candidate by selects -- unrolling the row loads, the distance and
+    // the list insert per candidate slot made this kernel ~15k instructions (instruction-cache
+    // misses) for no gain
+    auto need = [&](int r, float df) {
+        const double d = (double)df;
+        return !(r < 0 || r == self || d - err(d) > keep);
+    };
+    auto rerank = [&](int r) { topk_fixed_insert<KM>(dl, il, rdist64_q(q16, qx, ref + (int64_t)r * D, D), r); };
+    if constexpr (CACHE2) {
+        unsigned mask = 0;
+#pragma unroll
+        for (int i = 0; i < KC; i++) {
+            if (h0 && need(rc0[i], dc0[i])) mask |= 1u << i;
+            if (h1 && need(rc1[i], dc1[i])) mask |= 1u << (KC + i);
+        }
+        while (mask) {
+            const int bit = __builtin_ctz(mask);
+            mask &= mask - 1;
+            int r = rc0[0];
+#pragma unroll
+            for (int i = 0; i < KC; i++) {
+                r = bit == i ? rc0[i] : r;
+                r = bit == KC + i ? rc1[i] : r;
+            }
+            rerank(r);
+        }
+    }
+    for (int s = j + (CACHE2 ? 2 * MG : 0); s < nsplit; s += MG) {
         int rr[KC];
         float dd[KC];
+        load_split(s, rr, dd);
+        unsigned long long mask = 0;
 #pragma unroll
-        for (int i = 0; i < KC; i++) {
-            rr[i] = cand_i[o + i];
-            dd[i] = cand_d[o + i];
-        }
+        for (int i = 0; i < KC; i++)
+            if (need(rr[i], dd[i])) mask |= 1ull << i;
+        while (mask) {
+            const int bit = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            int r = rr[0];
 #pragma unroll
-        for (int i = 0; i < KC; i++) {
-            const double d = (double)dd[i];
-            if (rr[i] < 0 || rr[i] == self || d - err(d) > keep) continue;
-            topk_fixed_insert<KM>(dl, il, rdist64_q(q16, qx, ref + (int64_t)rr[i] * D, D), rr[i]);
+            for (int i = 1; i < KC; i++) r = bit == i ? rr[i] : r;
+            rerank(r);
         }
     }
 #pragma unroll
@@ -1024,8 +1073,93 @@ __global__ __launch_bounds__(64) void knn_merge(const double *__restrict__ ref, 
 }
 
 
-// exhaustive fp64 for the queries the screen could not certify: one workgroup per query
+// exhaustive fp64 for the queries the screen could not certify (fb_list[0 .. cnt)), in cand_less
+// order like every other stage.  Two roles in one launch (no host round trip to learn cnt):
+//  * blocks [0, nbp): the first FB_C listed queries, each query's reference rows cut into P parts
+//    of prow rows, ONE WAVE per part: every lane keeps the KM smallest of its rows in registers,
+//    the wave takes the part's k smallest by k rounds of a butterfly minimum (the winning lane
+//    pops its head), writes them to the workspace, and the wave that finishes a query's last part
+//    (a per-query counter, zeroed with the fallback count) merges the P lists the same way, one
+//    lane per part.  Round 5 scanned a query with one workgroup: the 3 fallback queries of the
+//    100k x 100k self-query on extracted features took 0.71-1.06 ms on 3 CUs.
+//  * blocks [nbp, grid): the listed queries past FB_C (only when a launch has that many), one
+//    workgroup per query: per-thread lists, then a tree merge through LDS.
 static constexpr int FB_T = 256;
+static constexpr int FB_C = 64;      // queries on the partitioned scan
+static constexpr int FB_PMAX = 64;   // parts per query (one lane per part in the final merge)
+static constexpr int FB_PROWS = 1024;  // target rows per part
+
+// the smallest (d, i) over the wave in cand_less order, on every lane
+__device__ __forceinline__ void wave_min_pair(double &d, int &i)
+{
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        const double od = __shfl_xor(d, m, 64);
+        const int oi = __shfl_xor(i, m, 64);
+        if (cand_less(od, oi, d, i)) {
+            d = od;
+            i = oi;
+        }
+    }
+}
+// k rounds: the wave's k smallest of the lanes' ascending KM-lists (consumed); lane j < k returns
+// the j-th in (od, oi)
+template <int KM>
+__device__ __forceinline__ void wave_take_k(double (&dl)[KM], int (&il)[KM], int k, int lane, double &od, int &oi)
+{
+    od = INFINITY;
+    oi = 0x7fffffff;
+    for (int j = 0; j < k; j++) {
+        double d = dl[0];
+        int i = il[0];
+        wave_min_pair(d, i);
+        if (lane == j) {
+            od = d;
+            oi = i;
+        }
+        if (dl[0] == d && il[0] == i && d < INFINITY) {  // this lane's head won: pop it
+#pragma unroll
+            for (int t = 0; t < KM - 1; t++) {
+                dl[t] = dl[t + 1];
+                il[t] = il[t + 1];
+            }
+            dl[KM - 1] = INFINITY;
+            il[KM - 1] = 0x7fffffff;
+        }
+    }
+}
+// idx / dist / pred of query q from the k results held by lanes 0 .. k-1
+template <int KM>
+__device__ __forceinline__ void fb_write(int64_t q, int k, int lane, double od, int oi, const int32_t *labels,
+                                         int32_t *idx, double *dist, int32_t *pred)
+{
+    const bool valid = od < INFINITY;
+    if (lane < k) {
+        idx[q * k + lane] = valid ? oi : -1;
+        dist[q * k + lane] = valid ? sqrt(od) : INFINITY;
+    }
+    if (pred && labels) {
+        const int lab = (lane < k && valid) ? labels[oi] : -1;
+        int best = -1, bestc = 0;
+#pragma unroll
+        for (int a = 0; a < KM; a++) {
+            if (a >= k) break;
+            const int la = __shfl(lab, a, 64);
+            if (la < 0) continue;
+            int cnt = 0;
+#pragma unroll
+            for (int b2 = 0; b2 < KM; b2++)
+                if (b2 < k) cnt += __shfl(lab, b2, 64) == la;
+            if (cnt > bestc || (cnt == bestc && la < best)) {
+                bestc = cnt;
+                best = la;
+            }
+        }
+        if (lane == 0) pred[q] = best;
+    }
+}
+
+template <int KM>
 __global__ __launch_bounds__(FB_T) void knn_fallback(const double *__restrict__ ref,
                                                      const double *__restrict__ query, int64_t Nr,
                                                      int D, int k, int64_t self_offset,
@@ -1033,67 +1167,121 @@ __global__ __launch_bounds__(FB_T) void knn_fallback(const double *__restrict__ 
                                                      const int32_t *__restrict__ labels,
                                                      int32_t *__restrict__ idx,
                                                      double *__restrict__ dist,
-                                                     int32_t *__restrict__ pred)
+                                                     int32_t *__restrict__ pred, int P, int64_t prow, int nbp,
+                                                     double *part_d, int *part_i, int *part_done)
 {
-    __shared__ double sd[FB_T / 2 * KMAX];
-    __shared__ int si[FB_T / 2 * KMAX];
     const int cnt = *fb_count;
-    const int tid = threadIdx.x;
-    for (int item = blockIdx.x; item < cnt; item += gridDim.x) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    if ((int)blockIdx.x < nbp) {  // ---- partitioned scan of the first FB_C listed queries
+        const int ncnt = min(cnt, FB_C);
+        const int nw = nbp * (FB_T / 64);
+        for (int u = (int)blockIdx.x * (FB_T / 64) + (tid >> 6); u < ncnt * P; u += nw) {
+            const int item = u / P, part = u - item * P;
+            const int64_t q = fb_list[item];
+            const double *qx = query + q * D;
+            const int64_t self = self_offset >= 0 ? self_offset + q : -1;
+            const int64_t r0 = (int64_t)part * prow, r1 = min(Nr, r0 + prow);
+            double dl[KM];
+            int il[KM];
+#pragma unroll
+            for (int i = 0; i < KM; i++) {
+                dl[i] = INFINITY;
+                il[i] = 0x7fffffff;
+            }
+            if (D <= 16) {  // two rows in flight per lane, the query in registers (four: 55.7 against
+                            // 46.6 us for the 3 fallbacks of the 100k self-query)
+                const QRow16 q16 = qrow16(qx, D);
+                for (int64_t r = r0 + lane; r < r1; r += 128) {
+                    double b[2][16];
+                    row16_load(b[0], ref + r * D, D);
+                    row16_load(b[1], ref + (r + 64 < r1 ? r + 64 : r) * D, D);
+                    if (r != self) topk_fixed_insert<KM>(dl, il, rdist64_16(q16, b[0], D), (int)r);
+                    if (r + 64 < r1 && r + 64 != self) topk_fixed_insert<KM>(dl, il, rdist64_16(q16, b[1], D), (int)(r + 64));
+                }
+            } else {
+                for (int64_t r = r0 + lane; r < r1; r += 64)
+                    if (r != self) topk_fixed_insert<KM>(dl, il, rdist64(qx, ref + r * D, D), (int)r);
+            }
+            double od;
+            int oi;
+            wave_take_k<KM>(dl, il, k, lane, od, oi);
+            const int64_t o = ((int64_t)item * P + part) * KM;
+            if (lane < k) {
+                part_d[o + lane] = od;
+                part_i[o + lane] = oi;
+            }
+            __threadfence();  // the part's list is visible device-wide (all XCDs) before it is counted
+            int last = 0;
+            if (lane == 0) last = atomicAdd(&part_done[item], 1) == P - 1;
+            if (!__shfl(last, 0, 64)) continue;
+            __threadfence();  // acquire: every part's list, from whichever XCD wrote it
+            // the final merge: lane p holds part p's ascending list
+#pragma unroll
+            for (int i = 0; i < KM; i++) {
+                const bool in = lane < P && i < k;
+                dl[i] = in ? part_d[((int64_t)item * P + lane) * KM + i] : INFINITY;
+                il[i] = in ? part_i[((int64_t)item * P + lane) * KM + i] : 0x7fffffff;
+            }
+            wave_take_k<KM>(dl, il, k, lane, od, oi);
+            fb_write<KM>(q, k, lane, od, oi, labels, idx, dist, pred);
+        }
+        return;
+    }
+    // ---- one workgroup per listed query past FB_C
+    __shared__ double sd[FB_T / 2 * KM];
+    __shared__ int si[FB_T / 2 * KM];
+    const int nbo = (int)gridDim.x - nbp;
+    for (int item = FB_C + (int)blockIdx.x - nbp; item < cnt; item += nbo) {
         const int64_t q = fb_list[item];
         const double *qx = query + q * D;
-        double dl[KMAX];
-        int il[KMAX];
+        const int64_t self = self_offset >= 0 ? self_offset + q : -1;
+        double dl[KM];
+        int il[KM];
 #pragma unroll
-        for (int i = 0; i < KMAX; i++) {
+        for (int i = 0; i < KM; i++) {
             dl[i] = INFINITY;
             il[i] = 0x7fffffff;
         }
-        if (D <= 16) {  // four rows in flight per thread, the query in registers
+        if (D <= 16) {
             const QRow16 q16 = qrow16(qx, D);
-            for (int64_t r0 = tid; r0 < Nr; r0 += 4 * FB_T) {
-                double b[4][16];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int64_t r = r0 + (int64_t)u * FB_T;
-                    row16_load(b[u], ref + (r < Nr ? r : 0) * D, D);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int64_t r = r0 + (int64_t)u * FB_T;
-                    if (r < Nr && !(self_offset >= 0 && r == self_offset + q))
-                        topk64_insert<KMAX>(dl, il, k, rdist64_16(q16, b[u], D), (int)r);
-                }
+            for (int64_t r = tid; r < Nr; r += FB_T) {
+                double b[16];
+                row16_load(b, ref + r * D, D);
+                if (r != self) topk_fixed_insert<KM>(dl, il, rdist64_16(q16, b, D), (int)r);
             }
         } else {
-            for (int64_t r = tid; r < Nr; r += FB_T) {
-                if (self_offset >= 0 && r == self_offset + q) continue;
-                topk64_insert<KMAX>(dl, il, k, rdist64(qx, ref + r * D, D), (int)r);
-            }
+            for (int64_t r = tid; r < Nr; r += FB_T)
+                if (r != self) topk_fixed_insert<KM>(dl, il, rdist64(qx, ref + r * D, D), (int)r);
         }
         // pairwise tree merge of the per-thread lists through LDS
         for (int width = FB_T; width > 1; width >>= 1) {
             const int half = width >> 1;
             __syncthreads();
             if (tid >= half && tid < width)
-                for (int i = 0; i < k; i++) {
-                    sd[(tid - half) * KMAX + i] = dl[i];
-                    si[(tid - half) * KMAX + i] = il[i];
+#pragma unroll
+                for (int i = 0; i < KM; i++) {
+                    sd[(tid - half) * KM + i] = dl[i];
+                    si[(tid - half) * KM + i] = il[i];
                 }
             __syncthreads();
             if (tid < half)
-                for (int i = 0; i < k; i++)
-                    topk64_insert<KMAX>(dl, il, k, sd[tid * KMAX + i], si[tid * KMAX + i]);
+#pragma unroll
+                for (int i = 0; i < KM; i++)
+                    if (i < k) topk_fixed_insert<KM>(dl, il, sd[tid * KM + i], si[tid * KM + i]);
         }
-        if (tid == 0) {
-            int outi[KMAX];
-            for (int i = 0; i < k; i++) {
-                const bool valid = dl[i] < INFINITY;
-                outi[i] = valid ? il[i] : -1;
-                idx[q * k + i] = outi[i];
-                dist[q * k + i] = valid ? sqrt(dl[i]) : INFINITY;
+        if (tid < 64) {  // wave 0: thread 0 holds the k smallest; spread them over lanes 0 .. k-1
+            double od = INFINITY;
+            int oi = 0x7fffffff;
+#pragma unroll
+            for (int i = 0; i < KM; i++) {
+                const double d = __shfl(dl[i], 0, 64);
+                const int ii = __shfl(il[i], 0, 64);
+                if (lane == i) {
+                    od = d;
+                    oi = ii;
+                }
             }
-            if (pred && labels) pred[q] = vote(outi, k, labels);
+            fb_write<KM>(q, k, lane, od, oi, labels, idx, dist, pred);
         }
         __syncthreads();
     }
@@ -1101,31 +1289,96 @@ __global__ __launch_bounds__(FB_T) void knn_fallback(const double *__restrict__ 
 
 // ---- z-score (src/feature_extraction.py:157-181), numpy axis-0 order ---------------------
 #pragma clang fp contract(off)
-// One wave per column: the rows are loaded 64 at a time (one per lane, all in flight together) and
-// added to the running sum in row order from the registers (wave-uniform, lane_read): numpy's
-// sequential axis-0 order exactly, without a dependent global load per row (round 5's one thread
-// per column: 46 ms for 100 000 x 15; the add chain itself is the floor).
-__global__ __launch_bounds__(64) void zscore_fit_kernel(const double *X, int64_t N, int D, double *mean, double *std)
+// numpy's axis-0 sums are sequential in row order per column, so each column is one dependent
+// chain of fp64 adds; the kernel's job is to keep that chain fed.  One workgroup per ZS_C columns:
+// waves 1-3 stage the next ZS_R-row tile of those columns in LDS (coalesced when the row is
+// narrower than ZS_C) while lane c of wave 0 adds the current tile's column c in row order from
+// LDS (reads issued ahead of the adds), then a barrier swaps the buffers.  Pass 0 sums x, pass 1
+// (x - mean)^2.  Round 5 ran one thread per column with a dependent global load per row (46 ms
+// for 100 000 x 15); one wave per column with lane_read 7.8 ms (v_readlane latency per add).
+static constexpr int ZS_T = 256, ZS_R = 256, ZS_C = 16;
+__global__ __launch_bounds__(ZS_T) void zscore_fit_kernel(const double *X, int64_t N, int D, double *mean, double *std)
 {
-    const int c = blockIdx.x, lane = threadIdx.x;
-    double s = 0.0;
-    for (int64_t b = 0; b < N; b += 64) {
-        const double x = b + lane < N ? X[(b + lane) * D + c] : 0.0;
-        const int cnt = (int)min((int64_t)64, N - b);
-        for (int j = 0; j < cnt; j++) s = s + lane_read(x, j);
+    __shared__ double tile[2][ZS_R * ZS_C];
+    const int c0 = (int)blockIdx.x * ZS_C, nc = min(ZS_C, D - c0), tid = threadIdx.x;
+    const int64_t ntile = (N + ZS_R - 1) / ZS_R;
+    // waves 1-3: rows [t ZS_R, +ZS_R) x columns [c0, c0 + nc), every load of the tile issued
+    // before the first LDS store (a store waits for its load: one at a time, a tile cost ~7 us)
+    constexpr int LPT = (ZS_R * ZS_C + ZS_T - 64 - 1) / (ZS_T - 64);
+    auto load = [&](int64_t t, int buf) {
+        double v[LPT];
+#pragma unroll
+        for (int u = 0; u < LPT; u++) {
+            const int e = tid - 64 + u * (ZS_T - 64);
+            const int r = e / nc, c = e - r * nc;
+            const int64_t row = t * ZS_R + r;
+            v[u] = (e < ZS_R * nc && row < N) ? X[row * D + c0 + c] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < LPT; u++) {
+            const int e = tid - 64 + u * (ZS_T - 64);
+            const int r = e / nc, c = e - r * nc;
+            if (e < ZS_R * nc) tile[buf][r * ZS_C + c] = v[u];
+        }
+    };
+    double m = 0.0, acc = 0.0;
+    for (int pass = 0; pass < 2; pass++) {
+        acc = 0.0;
+        if (tid >= 64) load(0, 0);
+        __syncthreads();
+        for (int64_t t = 0; t < ntile; t++) {
+            const int buf = (int)(t & 1);
+            if (tid >= 64) {
+                if (t + 1 < ntile) load(t + 1, buf ^ 1);
+            } else if (tid < nc) {
+                const int rows = (int)min((int64_t)ZS_R, N - t * ZS_R);
+                const double *col = tile[buf] + tid;
+                // batches of 8 rows, the next batch's 8 LDS reads issued before this batch's adds
+                // (16 reads ahead measured slower, 4.16 against 2.69 ms: the LDS counter holds at
+                // most 15 outstanding reads, so the first add waited for all of them)
+                auto add8 = [&](const double (&v)[8]) {
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        if (pass == 0) {
+                            acc = acc + v[u];
+                        } else {
+                            const double x = v[u] - m;
+                            acc = acc + x * x;
+                        }
+                    }
+                };
+                int r = 0;
+                if (rows >= 16) {
+                    double va[8], vb[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) va[u] = col[u * ZS_C];
+                    for (; r + 16 <= rows; r += 16) {
+#pragma unroll
+                        for (int u = 0; u < 8; u++) vb[u] = col[(r + 8 + u) * ZS_C];
+                        add8(va);
+                        const bool more = r + 24 <= rows;
+#pragma unroll
+                        for (int u = 0; u < 8; u++) va[u] = more ? col[(r + 16 + u) * ZS_C] : 0.0;
+                        add8(vb);
+                    }
+                }
+                for (; r < rows; r++) {
+                    if (pass == 0) {
+                        acc = acc + col[r * ZS_C];
+                    } else {
+                        const double x = col[r * ZS_C] - m;
+                        acc = acc + x * x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        if (pass == 0) m = acc / (double)N;
     }
-    const double m = s / (double)N;
-    double v = 0.0;
-    for (int64_t b = 0; b < N; b += 64) {
-        const double x = b + lane < N ? X[(b + lane) * D + c] - m : 0.0;
-        const double t2 = x * x;
-        const int cnt = (int)min((int64_t)64, N - b);
-        for (int j = 0; j < cnt; j++) v = v + lane_read(t2, j);
-    }
-    if (lane == 0) {
-        const double sd = sqrt(v / (double)N);
-        mean[c] = m;
-        std[c] = sd == 0.0 ? 1.0 : sd;
+    if (tid < nc) {
+        const double sd = sqrt(acc / (double)N);
+        mean[c0 + tid] = m;
+        std[c0 + tid] = sd == 0.0 ? 1.0 : sd;
     }
 }
 
@@ -1144,7 +1397,8 @@ __global__ void zscore_apply_kernel(const double *X, int64_t N, int D, const dou
 // ------------------------------------------------------------------------------------------
 namespace {
 struct KnnLayout {
-    size_t ref32, refmx, q32, cand_d, cand_i, misc, pilot_d, seed0, seed, total;
+    size_t ref32, refmx, q32, cand_d, cand_i, misc, fb_d, fb_i, pilot_d, seed0, seed, total;
+    int fb_parts, fb_km;  // partitioned fallback: parts per query, list length
     int DP, KC, nsplit;
     int rstride, nsample, nsplit_p;  // seeded thresholds (rstride > 0): sample rows j * rstride
     int rstride0, nsample0, nsplit_p0;  // the pilot's own seed: a smaller sample (rows j * rstride0)
@@ -1306,7 +1560,16 @@ KnnLayout knn_layout(int64_t Nr, int64_t Nq, int D, int k)
     l.q32 = o;   o += al((size_t)Nq * l.DP * 4);
     l.cand_d = o; o += al((size_t)l.nsplit * Nq * l.KC * 4);
     l.cand_i = o; o += al((size_t)l.nsplit * Nq * l.KC * 4);
-    l.misc = o;  o += al(16 + (size_t)Nq * 4);   // (unused), fallback count, fallback list
+    // (unused), fallback count, 2 words (unused), the per-query part counters of the partitioned
+    // fallback (FB_C words, zeroed with the count), the fallback list
+    l.misc = o;  o += al(16 + 4 * (size_t)dsp::FB_C + (size_t)Nq * 4);
+    l.fb_parts = (int)std::max<int64_t>(1, std::min<int64_t>(dsp::FB_PMAX, (Nr + dsp::FB_PROWS - 1) / dsp::FB_PROWS));
+    l.fb_km = k <= 8 ? 8 : k <= 16 ? 16 : 32;
+    {
+        const size_t nfb = (size_t)std::min<int64_t>(Nq, dsp::FB_C) * l.fb_parts * l.fb_km;
+        l.fb_d = o; o += al(nfb * 8);
+        l.fb_i = o; o += al(nfb * 4);
+    }
     l.pilot_d = l.seed0 = l.seed = 0;
     if (l.rstride) {
         // pilot splits: enough workgroups to fill the chip twice over, >= one tile of rows each
@@ -1419,9 +1682,10 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
     int *ci = (int *)(ws + l.cand_i);
     unsigned *mx = (unsigned *)(ws + l.refmx);
     int *fbc = (int *)(ws + l.misc + 4);
-    int *fbl = (int *)(ws + l.misc + 16);
+    int *fbdone = (int *)(ws + l.misc + 16);
+    int *fbl = (int *)(ws + l.misc + 16 + 4 * dsp::FB_C);
     float *seedp = l.rstride ? (float *)(ws + l.seed) : nullptr;
-    if (hipMemsetAsync(ws + l.misc, 0, 16, s) != hipSuccess) return DSP_ERR_HIP;
+    if (hipMemsetAsync(ws + l.misc, 0, 16 + 4 * dsp::FB_C, s) != hipSuccess) return DSP_ERR_HIP;
     const int cb = 256;
     if (Nr > 0 && !(flags & DSP_KNN_REF_READY)) {  // (fit: the reference set in fp32 + its max norm)
         if (hipMemsetAsync(mx, 0, 4, s) != hipSuccess) return DSP_ERR_HIP;
@@ -1531,9 +1795,22 @@ extern "C" int dsp_knn_classify(const double *ref, const int32_t *ref_labels, in
     default: merged = launch_merge<36>(s, ref, query, Nr, Nq, D, k, l.nsplit, self_offset, cd, ci, mx, er, ea, lbl, idx, dist, pred, fbc, fbl, seedp); break;
     }
     if (!merged) return DSP_ERR_ARGS;  // unreachable while KC >= k + KNN_SLACK (knn_layout)
-    const unsigned fbgrid = (unsigned)(Nq < 512 ? Nq : 512);
-    hipLaunchKernelGGL(dsp::knn_fallback, dim3(fbgrid), dim3(dsp::FB_T), 0, s, ref, query, Nr, D,
-                       k, self_offset, fbc, fbl, lbl, idx, dist, pred);
+    {
+        // partitioned role: enough waves for every part of FB_C queries, at most 1 024 (most
+        // launches list no query and these workgroups return at once); the per-workgroup role only
+        // when this launch can list more than FB_C queries
+        const int P = l.fb_parts;
+        const int64_t prow = (Nr + P - 1) / P;
+        const int nbp = (int)std::min<int64_t>(256, ((int64_t)std::min<int64_t>(Nq, dsp::FB_C) * P + 3) / 4);
+        const int nbo = Nq > dsp::FB_C ? (int)std::min<int64_t>(512, Nq - dsp::FB_C) : 0;
+        double *fbd = (double *)(ws + l.fb_d);
+        int *fbi = (int *)(ws + l.fb_i);
+#define DSP_FB(KMV)                                                                                              \
+    hipLaunchKernelGGL((dsp::knn_fallback<KMV>), dim3((unsigned)(nbp + nbo)), dim3(dsp::FB_T), 0, s, ref, query, Nr, \
+                       D, k, self_offset, fbc, fbl, lbl, idx, dist, pred, P, prow, nbp, fbd, fbi, fbdone)
+        if (l.fb_km == 8) DSP_FB(8); else if (l.fb_km == 16) DSP_FB(16); else DSP_FB(32);
+#undef DSP_FB
+    }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? DSP_OK : DSP_ERR_HIP + (int)e;
 }
@@ -1542,8 +1819,8 @@ extern "C" int dsp_zscore_fit(const double *X, int64_t N, int D, double *mean, d
                               void *stream)
 {
     if (!X || !mean || !std || N < 1 || D < 1) return DSP_ERR_ARGS;
-    hipLaunchKernelGGL(dsp::zscore_fit_kernel, dim3((unsigned)D), dim3(64), 0, (hipStream_t)stream, X, N, D, mean,
-                       std);
+    hipLaunchKernelGGL(dsp::zscore_fit_kernel, dim3((unsigned)((D + dsp::ZS_C - 1) / dsp::ZS_C)), dim3(dsp::ZS_T), 0,
+                       (hipStream_t)stream, X, N, D, mean, std);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? DSP_OK : DSP_ERR_HIP + (int)e;
 }

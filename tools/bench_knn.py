@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--cpu-queries", type=int, default=200)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="also time the query job replayed from a HIP graph")
     ap.add_argument("--data", choices=("extracted", "synthetic"), default="extracted",
                     help="extracted: the z-scored 15-d features of --ref synthetic utterances (BASELINE "
                          "configs[4]); synthetic: Gaussian vectors around 10 class centres (rounds 1-5)")
@@ -78,11 +79,35 @@ def main():
         times.append(e0.elapsed_time(e1) / 1e3)
     st = {}  # the fallback count reads the workspace (a host sync): one untimed call
     index.query(Qd, self_offset=q0, stats=st)
+    t_graph = None
+    if a.graph:  # the same query job captured once and replayed (launch gaps gone: serving use)
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            index.query(Qd, self_offset=q0)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            gi, gd, gp = index.query(Qd, self_offset=q0)
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(gi, idx) and torch.equal(gd, dist) and (gp is None or torch.equal(gp, pred))
+        gt = []
+        for _ in range(a.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            gt.append(e0.elapsed_time(e1) / 1e3)
+        t_graph = float(np.median(gt))
     t = float(np.median(times))
     pairs = float(a.ref) * a.queries
     res = {"metric": "k-NN pairs/s (15-d, exact, KNeighborsClassifier semantics)",
            "value": round(pairs / t, 1), "unit": "pairs/s", "ms": round(t * 1e3, 4),
            "fallbacks": st.get("fallbacks"),
+           "ms_graph_replay": None if t_graph is None else round(t_graph * 1e3, 4),
            "config": {"ref": a.ref, "queries": a.queries, "dim": a.dim, "k": a.k, "self_query": True,
                       "data": ("z-scored 15-d features of %d synthetic utterances (fused extraction + "
                                "normalize_features on the device), labels i mod 10" % a.ref)

@@ -30,7 +30,7 @@ if [[ " $S " == *" rehearsal "* ]]; then
 fi
 if [[ " $S " == *" knn "* ]]; then
   for q in 12500 100000; do
-    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/knn_$q -o kt -- python3 $R/tools/bench_knn.py --queries $q --no-cpu > $O/knn_$q.json 2> $O/knn_$q.err) || { tail -5 $O/knn_$q.err; exit 1; }
+    (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/knn_$q -o kt -- python3 $R/tools/bench_knn.py --queries $q --no-cpu --graph > $O/knn_$q.json 2> $O/knn_$q.err) || { tail -5 $O/knn_$q.err; exit 1; }
     tail -1 $O/knn_$q.json | cut -c1-300
   done
 fi
