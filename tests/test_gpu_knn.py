@@ -199,10 +199,14 @@ def test_knn_seeded_screen_vs_oracle(k):
     assert np.array_equal(p1.cpu().numpy(), p0)
 
 
-def test_knn_adversarially_tight_seed_falls_back_exactly(monkeypatch):
+@pytest.mark.parametrize("k", [5, 12, 25])
+def test_knn_adversarially_tight_seed_falls_back_exactly(monkeypatch, k):
     """The diagnostic build scales every seed by DSP_KNN_SEED_SCALE: at 0.25 the seeds sit below
     the true k-th distance, the screen keeps too few rows, certification fails, and the exhaustive
-    fallback must still return the oracle's exact answer (self-query and foreign queries)."""
+    fallback must still return the oracle's exact answer (self-query and foreign queries).  Over
+    300 listed queries run both roles of knn_fallback: the first 64 on the partitioned scan (40
+    parts of 1 000 rows, one wave each, merged by the last wave), the rest one workgroup each;
+    k = 5 / 12 / 25 instantiate its 8-, 16- and 32-entry lists."""
     from src.pipeline import knn_classify
     rng = np.random.default_rng(77)
     X, y = _clustered(rng, 40000, 15)
@@ -211,17 +215,43 @@ def test_knn_adversarially_tight_seed_falls_back_exactly(monkeypatch):
 
     def run():
         st1, st2 = {}, {}
-        a = knn_classify(X, y, Q, 5, stats=st1)
-        b = knn_classify(X, y, X[100:700], 5, self_offset=100, stats=st2)
+        a = knn_classify(X, y, Q, k, stats=st1)
+        b = knn_classify(X, y, X[100:700], k, self_offset=100, stats=st2)
         return a, b, st1, st2
     (i1, d1, p1), (j1, e1, q1), st1, st2 = _with_library("knndiag", run)
     assert st1["fallbacks"] > 300 and st2["fallbacks"] > 300, (st1, st2)
-    i0, d0, p0 = oracle.knn(X, y, Q, 5, n_classes=10, nthreads=16)
+    i0, d0, p0 = oracle.knn(X, y, Q, k, n_classes=10, nthreads=16)
     assert np.array_equal(i1.cpu().numpy(), i0) and np.array_equal(d1.cpu().numpy(), d0)
     assert np.array_equal(p1.cpu().numpy(), p0)
-    j0, e0, q0 = oracle.knn(X, y, X[100:700], 5, n_classes=10, self_offset=100, nthreads=16)
+    j0, e0, q0 = oracle.knn(X, y, X[100:700], k, n_classes=10, self_offset=100, nthreads=16)
     assert np.array_equal(j1.cpu().numpy(), j0) and np.array_equal(e1.cpu().numpy(), e0)
     assert np.array_equal(q1.cpu().numpy(), q0)
+
+
+@pytest.mark.parametrize("D,k", [(40, 7), (24, 20), (15, 3)])
+def test_knn_fallback_duplicates_across_parts(D, k):
+    """Twenty exact copies of every base row, spread over the whole reference set (np.tile), so a
+    query's tied neighbours sit in many parts of the partitioned fallback scan: the parts' lists
+    and their merge must keep the reference's (distance, index) order across parts.  D = 40 / 24
+    take the direct-form screens and the fallback's general distance loop, D = 15 the register
+    path.  Bit-exact against the oracle, foreign queries and a self-query block."""
+    from src.pipeline import knn_classify
+    rng = np.random.default_rng(D * 100 + k)
+    base = rng.standard_normal((1000, D))
+    X = np.tile(base, (20, 1))  # row i copies base[i % 1000]: copies 1 000 rows apart
+    y = rng.integers(0, 10, X.shape[0]).astype(np.int32)
+    Q = base[:120] + 1e-9
+    st = {}
+    i1, d1, p1 = knn_classify(X, y, Q, k, stats=st)
+    i0, d0, p0 = oracle.knn(X, y, Q, k, n_classes=10, nthreads=16)
+    assert np.array_equal(i1.cpu().numpy(), i0) and np.array_equal(d1.cpu().numpy(), d0)
+    assert np.array_equal(p1.cpu().numpy(), p0)
+    print("duplicates across parts D=%d k=%d: %d of 120 queries fell back" % (D, k, st["fallbacks"]))
+    lo = 5000
+    i1, d1, p1 = knn_classify(X, y, X[lo:lo + 150], k, self_offset=lo)
+    i0, d0, p0 = oracle.knn(X, y, X[lo:lo + 150], k, n_classes=10, self_offset=lo, nthreads=16)
+    assert np.array_equal(i1.cpu().numpy(), i0) and np.array_equal(d1.cpu().numpy(), d0)
+    assert np.array_equal(p1.cpu().numpy(), p0)
 
 
 def test_knn_kc6_duplicates_and_ties_fall_back_exactly():
