@@ -39,6 +39,7 @@
 #include "dsp_audiorec.h"
 #include "extract_layout.h"
 #include "dsp_device.h"
+#include "crop.h"
 
 #ifndef DSP_ABL  // the phase-ablation instrument (tools/ablate_build.sh, diagnostic builds only;
 #define DSP_ABL 0 // outputs are wrong): skip 1 = R4 frames, 2 = R5 jobs, 4 = R2 sign bits,
@@ -185,7 +186,7 @@ __device__ __forceinline__ ClipRef clip_none()
 
 struct Ctx {
     Shared *sh;
-    const float *wtab;  // EXTRACT_WROW(L) floats per shifted copy r = 0..3 (extract_layout.h)
+    const float *wtab;  // 2 copies of EXTRACT_WROW(L) (w^2, |w|) pairs, shifted by 0 / 1 (build_window)
     uint32_t *posw;      // bit u of the buffer: sample u is real and positive after preprocess
     unsigned long long *wS2;
     int *wS1;
@@ -193,6 +194,7 @@ struct Ctx {
     int32_t *vZ;
     float *fE, *fM;
     int32_t *fZ;
+    float *parts;  // R4a's unit partials (crop_plan), over wS2 / wS1
     int *rank;  // rank scratch: nvcap or 3 * fcap ints
     int *pS1;   // partial-word moments at the two ends of each VAD frame (2 * nvcap)
     unsigned long long *pS2;
@@ -867,118 +869,166 @@ __device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur
     }
 }
 
-// R4: windowed frames over the crop [st, en) (:378, :299-333; fe.py:12-43) -> c.fE / fM / fZ.
-// One 16-lane row per frame (4 frames per wave), in the canonical order of dsp_device.h: the
-// frame's clip-relative 8-sample vectors are re-read from L2 (16-B loads at the clip's own 2-byte
-// alignment) and lane rl takes vectors va + rl + 16k, so the sums do not depend on where the clip
-// sits in the buffer and equal dsp_extract_general's.  Per sample y = w_j x (the reference's
-// windowed frame, :329-331), E += y^2, M += |y|; the weights of a vector's 8 samples are two
-// aligned 16-B reads from the window copy shifted by fs mod 4.  Returns F.
-// vectors per lane in one batch from L2: 7 (896 samples per row) leaves the FAST kernel without
-// VGPR spills; 9 (a whole 1102-sample frame) 2.71 ms, 7 2.65 ms, 6 / 8 2.61-2.64 / 2.66-2.68 ms at
-// 100k clips (profiles/r05s_ab_prefetch_kv.txt, r05kv_ab_r4_batch.txt)
-static constexpr int R4_KV = 7;
-__device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int L, int S,
-                                         int st, int en, const ClipStats &cs, int j0, int j1, int wrank, int lane)
+// R4: windowed frames over the crop [st, en) (:378, :299-333; fe.py:12-43).  E and M as the
+// blocked product of dsp_device.h (crop_plan: the crop's S-sample blocks against the window's
+// D = ceil(L / S) S-sample slices) on the matrix cores, the ZCR per frame from the positive bits.
+// (Rounds 2-6 summed each frame on its own: one 16-lane row per frame re-read the frame's 16-B
+// vectors from L2 and converted, centred and weighted every sample once per frame it lies in,
+// 2.5 times on average at 1102 / 441: ~7.5 VALU per sample pair and frame, 3.1k VALU per clip.)
+static constexpr int crop_frames(int m, int L, int S) { return (m <= L) ? 1 : (m - L + S - 1) / S + 1; }
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// R4a: the unit partials of the crop (dsp_device.h crop_plan) -> parts.  Wave w takes units
+// 16 w + beta, beta = lane / 4 (one v_mfma_f32_4x4x1f32 block each, 16 per instruction); lane
+// (beta, l4 = lane % 4) supplies weight row 4 g + l4 and data column l4 (block 4 q + l4) of its unit
+// and ends holding that column's partials of the four rows.  A step is one sample per lane: its x^2
+// and |x| against (w^2, |w|), two MFMAs, alternating between two chains per quantity (even / odd
+// steps).  Steps come in chunks of 8: one 16-B load of the lane's 8 samples (the clip's own 2-byte
+// alignment, from L2) and four 16-B LDS reads of the 8 weight pairs.  Every lane runs the loop
+// (wave-uniform control flow around the MFMAs); lanes past the last unit compute unused partials.
+__device__ __forceinline__ void r4_units(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int L, int S,
+                                         int st, int en, const ClipStats &cs, const CropPlan &cp, int wid, int lane)
 {
-    const int n = cur.n, lead = cur.lead;
-    const int m = en - st;  // > 0 always (start < end)
-    const int F = (m <= L) ? 1 : (m - L + S - 1) / S + 1;
-    const float sE = cs.invMf * cs.invMf, sM = cs.invMf;
-    const int wrow = EXTRACT_WROW(L);
+    const int units = cp.nq * cp.P;
     const CanonX cx = canon_x(cs.mq, cs.t0);
-    // a 16-B load ending past the clip's last buffer vector drops a dword that straddles the
-    // descriptor's end (range checks are per dword): with an odd lead and a clip ending on a
-    // vector boundary that dword holds the last sample, patched in from the aligned vector
-    const int vfix = ((lead & 1) && ((lead + n) & 7) == 0) ? (n - 1) >> 3 : -1;
-    const short klast = vfix >= 0 ? load_vec(p, cur, cur.nvec - 1)[7] : (short)0;
-    auto frame_vec = [&](auto padded_t, auto near_t, const short8 &x8, const float *wr, int jb, int lim,
-                         float2v &ea, float &m0, float &m1) {
-        constexpr bool PADDED = decltype(padded_t)::value, NEAR0 = decltype(near_t)::value;
-        const float4 wa = *reinterpret_cast<const float4 *>(wr + jb);
-        const float4 wb = *reinterpret_cast<const float4 *>(wr + jb + 4);
-        const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+    const int beta = lane >> 2, l4 = lane & 3;
+    const __amdgpu_buffer_rsrc_t rs = clip_rsrc(p, cur);
+    const int n = cur.n, lead = cur.lead, wrow = EXTRACT_WROW(L);
+    // a 16-B load at an odd sample position drops its last dword when that dword straddles the
+    // clip's range end (range checks are per dword): when the clip ends on a vector boundary that
+    // dword holds the clip's last sample, patched in from an aligned load
+    const bool vfix = ((lead + n) & 7) == 0;
+    const int klast = vfix ? (int)(short)__builtin_amdgcn_raw_buffer_load_b16(rs, 2 * (lead + n - 1), 0, 0) : 0;
+    const float2 *wt = reinterpret_cast<const float2 *>(c.wtab);
+    for (int u0 = 16 * wid; u0 < units; u0 += 16 * NWAVE) {
+        const int u = u0 + beta;
+        const bool live = u < units;
+        const int q = live ? u / cp.P : 0, pp = live ? u - q * cp.P : 0;
+        const int t0 = pp * cp.T;
+        const int cs0 = st + (4 * q + l4) * S + t0;                      // clip sample of step 0
+        const int lim = live ? min(min(cp.T, S - t0), en - cs0) : cp.T;  // steps with data (then 0)
+        for (int g = 0; g < cp.NG; g++) {
+            const int j0 = (4 * g + l4) * S + t0;  // window index of step 0 (the lane's weight row)
+            f4v e0 = {0.f, 0.f, 0.f, 0.f}, e1 = e0, m0 = e0, m1 = e0;
+            short8 nxt = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rs, 2 * (lead + cs0), 0, 0));
+            for (int k = 0; k < cp.T; k += 8) {
+                const short8 raw = nxt;
+                if (k + 8 < cp.T)
+                    nxt = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rs, 2 * (lead + cs0 + k + 8), 0, 0));
+                // data: x of the lane's 8 samples, 0 past its steps (the part's end, the crop's end)
+                float2v xv[4];
+                const int rem = lim - k;
+                if (__builtin_expect(__ballot(rem < 8 || (vfix && rem == 8)) != 0, 0)) {
+                    const int cs = cs0 + k;
+                    short8 r = raw;
+                    if (vfix && ((lead + cs) & 1) && n - 1 >= cs && n - 1 < cs + 8) r[(n - 1 - cs) & 7] = (short)klast;
 #pragma unroll
-        for (int h = 0; h < 4; h++) {
-            float2v w = {wv[2 * h], wv[2 * h + 1]};
-            if (PADDED) {  // samples past the crop are zero padding
-                const int j = jb + 2 * h;  // window index of the pair's first sample
-                w.x = j < lim ? w.x : 0.f;
-                w.y = j + 1 < lim ? w.y : 0.f;
+                    for (int h = 0; h < 4; h++) {
+                        xv[h] = canon_x2<false>(r[2 * h], r[2 * h + 1], cx);
+                        xv[h].x = 2 * h < rem ? xv[h].x : 0.f;
+                        xv[h].y = 2 * h + 1 < rem ? xv[h].y : 0.f;
+                    }
+                } else {
+#pragma unroll
+                    for (int h = 0; h < 4; h++) xv[h] = canon_x2<false>(raw[2 * h], raw[2 * h + 1], cx);
+                }
+                // weight pairs j .. j + 7, in two halves (zero past L; the copy shifted by j's
+                // parity is 16-B aligned)
+                const int jj = j0 + k;
+                const float4 *src = reinterpret_cast<const float4 *>(wt + (jj & 1) * wrow + jj + (jj & 1));
+#pragma unroll
+                for (int hh = 0; hh < 2; hh++) {
+                    float4 wa = {0.f, 0.f, 0.f, 0.f}, wb = wa;
+                    if (jj < L) {
+                        wa = src[2 * hh];
+                        wb = src[2 * hh + 1];
+                    }
+                    const float w2[4] = {wa.x, wa.z, wb.x, wb.z}, aw[4] = {wa.y, wa.w, wb.y, wb.w};
+                    float x2[4], ax[4];
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const float2v xx = xv[2 * hh + h];
+                        const float2v sq = xx * xx;  // (no contraction: separate products)
+                        x2[2 * h] = sq.x;
+                        x2[2 * h + 1] = sq.y;
+                        ax[2 * h] = fabsf(xx.x);
+                        ax[2 * h + 1] = fabsf(xx.y);
+                    }
+#pragma unroll
+                    for (int s4 = 0; s4 < 4; s4++) {
+                        const int s = 4 * hh + s4;
+                        if (k + s < cp.T) {  // wave-uniform
+                            if (s & 1) {
+                                e1 = __builtin_amdgcn_mfma_f32_4x4x1f32(w2[s4], x2[s4], e1, 0, 0, 0);
+                                m1 = __builtin_amdgcn_mfma_f32_4x4x1f32(aw[s4], ax[s4], m1, 0, 0, 0);
+                            } else {
+                                e0 = __builtin_amdgcn_mfma_f32_4x4x1f32(w2[s4], x2[s4], e0, 0, 0, 0);
+                                m0 = __builtin_amdgcn_mfma_f32_4x4x1f32(aw[s4], ax[s4], m0, 0, 0, 0);
+                            }
+                        }
+                    }
+                }
             }
-            canon_pair(w, canon_x2<NEAR0>(x8[2 * h], x8[2 * h + 1], cx), ea, m0, m1);
+            if (live) {
+                f4v se, sm;
+                {
+#pragma clang fp contract(off)
+                    se = e0 + e1;
+                    sm = m0 + m1;
+                }
+                *reinterpret_cast<f4v *>(c.parts + crop_part_index(cp, 0, u, g, l4, 0)) = se;
+                *reinterpret_cast<f4v *>(c.parts + crop_part_index(cp, 1, u, g, l4, 0)) = sm;
+            }
         }
-    };
-    constexpr int KV = R4_KV;
+    }
+}
+
+// R4z: the ZCR of each frame of the crop (fe.py:34-40) -> c.fZ: one 16-lane row per frame, 4 per
+// wave.  A sample's sign survives windowing where w_j > 0 (j in [j0, j1]) and j < lim; transitions
+// into the window's zero ends / padding count too.
+__device__ __forceinline__ void r4_zcr(const Ctx &c, const ClipRef &cur, int L, int S, int st, int en, int F, int j0,
+                                       int j1, int wrank, int lane)
+{
+    const int lead = cur.lead;
     const int rl = lane & 15, row = lane >> 4;
     for (int gi = wrank; !(DSP_ABL & 1) && 4 * gi < F; gi += NWAVE) {
         const int g = 4 * gi + row;
         const bool act = g < F;
-        const int gc = act ? g : F - 1;
-        const int fs = st + gc * S;
-        const int lim = min(L, en - fs);  // samples beyond the crop are zero padding
-        const bool padded = lim < L;
-        const int va = fs >> 3, vb = (fs + lim - 1) >> 3;
-        const int r = fs & 3;  // copy whose rows start at window index = -fs (mod 4)
-        const float *wr = c.wtab + r * wrow + EXTRACT_WPAD + r;  // wr[j] = w[j], j = -7 .. L + 7
-        float2v ea = {0.f, 0.f};
-        float m0 = 0.f, m1 = 0.f;
-        for (int v0 = va; v0 <= vb; v0 += 16 * KV) {
-            // the lane's vectors v0 + rl + 16k: one per-lane base (vl) and immediate offsets, a
-            // per-lane bound (vlim) against uniform 16k -- nine hoisted per-k indices spilled at
-            // 80 VGPRs and every reload waited for all of the batch's loads
-            const int vl = v0 + rl, vlim = vb - vl;
-            short8 xv[KV];
-#pragma unroll
-            for (int k = 0; k < KV; k++) xv[k] = load_cvec(p, cur, vl + 16 * k);
-            if (vfix >= 0)  // clip-uniform, rare
-#pragma unroll
-                for (int k = 0; k < KV; k++)
-                    if (vl + 16 * k == vfix) xv[k][(n - 1) & 7] = klast;
-            const int jl = 8 * vl - fs;  // window index of the lane's first vector
-            auto run = [&](auto pt, auto nt) {
-#pragma unroll
-                for (int k = 0; k < KV; k++)
-                    if (16 * k <= vlim) frame_vec(pt, nt, xv[k], wr, jl + 128 * k, lim, ea, m0, m1);
-            };
-            if (padded)
-                cx.near0 ? run(BoolT<true>(), BoolT<true>()) : run(BoolT<true>(), BoolT<false>());
-            else if (cx.near0)
-                run(BoolT<false>(), BoolT<true>());
-            else
-                run(BoolT<false>(), BoolT<false>());
-        }
-        const float E1 = dpp_row_reduce(ea.x + ea.y, OpAdd()) * sE;
-        const float M1 = dpp_row_reduce(m0 + m1, OpAdd()) * sM;
-        // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in
-        // [j0, j1]) and j < lim; transitions into the window's zero ends / padding count too
+        const int fs = st + (act ? g : F - 1) * S;
         const int ia = fs + j0, ib = min(fs + j1, en - 1);  // sample coords
         int z = dpp_row_reduce(ia < ib ? chg_count(c.posw, ia + lead, ib + lead, rl, 16) : 0, OpAdd());
         if (ia <= ib) {
             if (j0 > 0) z += pos_bit(c.posw, ia + lead);
             if (ib < fs + L - 1) z += pos_bit(c.posw, ib + lead);
         }
-        if (act && rl == 0) {
-            c.fE[g] = E1;
-            c.fM[g] = M1;
-            c.fZ[g] = z;
-        }
+        if (act && rl == 0) c.fZ[g] = z;
     }
-    return F;
 }
 
 // R5 for F <= 128 (compute_statistics x 3, fe.py:46-62): six jobs on waves 0..5 -- wave q (q < 3)
 // the median of sequence q (E, M, ZCR) by an in-wave bitonic sort, wave 3 + q its mean /
 // population std (fp64 sums) / max / min -- no barrier.  np.median: the middle order statistic
 // (odd F) or the mean of the two middle ones.
-__device__ __forceinline__ void r5_fast(const Ctx &c, int F, float *featb, int wid, int lane)
+// E / M of frame j come from R4a's unit partials (crop_frame_sum, times invMf^2 / invMf); with
+// `keep` (the per-frame sequence is an output) the statistics waves also store them to c.fE / fM.
+__device__ __forceinline__ void r5_fast(const Ctx &c, int F, const CropPlan &cp, float invMf, bool keep,
+                                        float *featb, int wid, int lane)
 {
     const int r0 = (F - 1) / 2, r1 = F / 2;
+    const float sE = invMf * invMf, sM = invMf;
     for (int job = wid; !(DSP_ABL & 2) && job < 6; job += NWAVE) {
         const int q = job % 3;
-        auto get = [&](int j) -> float { return q == 0 ? c.fE[j] : q == 1 ? c.fM[j] : (float)c.fZ[j]; };
+        auto get = [&](int j) -> float {
+            return q == 0 ? crop_frame_sum(c.parts, cp, j, 0) * sE
+                          : q == 1 ? crop_frame_sum(c.parts, cp, j, 1) * sM : (float)c.fZ[j];
+        };
         const bool in0 = lane < F, in1 = lane + 64 < F;
         const float x0 = in0 ? get(lane) : 0.f, x1 = in1 ? get(lane + 64) : 0.f;
+        if (keep && job >= 3 && q < 2) {
+            float *dst = q == 0 ? c.fE : c.fM;
+            if (in0) dst[lane] = x0;
+            if (in1) dst[lane + 64] = x1;
+        }
         if (job < 3) {  // median by an in-wave bitonic sort
             unsigned a[2] = {in0 ? fkey(x0) : ~0u, in1 ? fkey(x1) : ~0u};
             float v0, v1;
@@ -1375,14 +1425,24 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     }
     STAMP(i, 4);
 
-    // ---- R4: windowed frames over the crop [st, en) (r4_frames) --------------------------------
-    const int F = r4_frames(p, c, cur, L, S, st, en, cs, sh->j0, sh->j1, wid, lane);
+    // ---- R4: windowed frames over the crop [st, en) (r4_units, r4_zcr) ------------------------
+    const int F = crop_frames(en - st, L, S);
+    const CropPlan cp = crop_plan(F, L, S);
+    r4_units(p, c, cur, L, S, st, en, cs, cp, wid, lane);
+    r4_zcr(c, cur, L, S, st, en, F, sh->j0, sh->j1, wid, lane);
     STAMP(i, 12);
-    if (!FAST && F > 128)
-        for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
     if constexpr (!EXACT)
         if (tid == 0) sh->next = resolve();  // claimed at the clip's start (-1: none)
     __syncthreads();
+    if (!FAST && F > 128) {  // long sequences: E / M materialised for the rank passes
+        const float sE = cs.invMf * cs.invMf, sM = cs.invMf;
+        for (int t = tid; t < F; t += NT) {
+            c.fE[t] = crop_frame_sum(c.parts, cp, t, 0) * sE;
+            c.fM[t] = crop_frame_sum(c.parts, cp, t, 1) * sM;
+        }
+        for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
+        __syncthreads();
+    }
     if constexpr (!EXACT) {
         // regs are dead since R2: the next clip's words load while R5 runs (unconditional, a
         // clip_none() reads zeros, so the compiler's vmcnt bookkeeping stays exact)
@@ -1396,7 +1456,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     const int r0 = (F - 1) / 2, r1 = F / 2;
     {
         if (FAST || F <= 128) {
-            r5_fast(c, F, featb, wid, lane);
+            r5_fast(c, F, cp, cs.invMf, p.seq != nullptr, featb, wid, lane);
         } else {  // long sequences: partial ranks over all waves, then one wave per sequence
             rank_partial([&](int q, int j) { return q == 2 ? (float)c.fZ[j] : (q == 0 ? c.fE[j] : c.fM[j]); },
                          3, F, c.rank, wid, lane);
@@ -1442,13 +1502,15 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
         }
     }
     STAMP(i, 9);
-    if (p.seq)
+    if (p.seq) {
+        __syncthreads();  // c.fE / fM of r5_fast's statistics waves
         for (int g = tid; g < F && g < p.ld_seq; g += NT) {
             float *o = p.seq + ((size_t)i * p.ld_seq + g) * 3;
             o[0] = c.fE[g];
             o[1] = c.fM[g];
             o[2] = (float)c.fZ[g];
         }
+    }
     if (tid == 0) {
         if constexpr (EXACT) {
             out_se(p, i)[0] = st;
@@ -1620,14 +1682,19 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
 
     // ---- R4: windowed frames over the crop [st, en) (r4_frames) --------------------------------
     MARK(R4);
-    const int F = r4_frames(p, c, cur, L, S, st, en, cs, sh->j0, sh->j1, wid, lane);
+    const int F = crop_frames(en - st, L, S);
+    const CropPlan cp = crop_plan(F, L, S);
+    r4_units(p, c, cur, L, S, st, en, cs, cp, wid, lane);
+    MARK(R4z);
+    r4_zcr(c, cur, L, S, st, en, F, sh->j0, sh->j1, wid, lane);
     STAMP(i, 12);
     __syncthreads();
     STAMP(i, 5);
 
     // ---- R5: 15-d statistics (compute_statistics x 3, fe.py:46-62) ------------------------
     MARK(R5);
-    r5_fast(c, F, featb, wid, lane);
+    const ExtractParams &qs = p;
+    r5_fast(c, F, cp, cs.invMf, qs.seq != nullptr, featb, wid, lane);
     if (wid == NWAVE - 1) {
         // idle in R5: the next clip's offsets to LDS, so that the loop top does not wait for a global
         // load (nor, through the in-order vmcnt, for the flushed output stores before it)
@@ -1637,14 +1704,15 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     }
     STAMP(i, 9);
     MARK(tail);
-    const ExtractParams &qs = p;
-    if (qs.seq)
+    if (qs.seq) {
+        __syncthreads();  // c.fE / fM of r5_fast's statistics waves
         for (int g = tid; g < F && g < qs.ld_seq; g += NT) {
             float *o = qs.seq + ((size_t)i * qs.ld_seq + g) * 3;
             o[0] = c.fE[g];
             o[1] = c.fM[g];
             o[2] = (float)c.fZ[g];
         }
+    }
     if (tid == 0) {
         int32_t *orow = c.orow + DSP_OUT_ROW_WORDS * oslot;
         orow[15] = st;
@@ -1686,6 +1754,7 @@ __device__ __forceinline__ Ctx ctx_from(const ExtractCarve &cv, unsigned char *l
     c.fE = reinterpret_cast<float *>(lds + cv.fE);
     c.fM = reinterpret_cast<float *>(lds + cv.fM);
     c.fZ = reinterpret_cast<int32_t *>(lds + cv.fZ);
+    c.parts = reinterpret_cast<float *>(lds + cv.parts);
     c.rank = reinterpret_cast<int *>(lds + cv.rank);
     c.pS1 = reinterpret_cast<int *>(lds + cv.pS1);
     c.pS2 = reinterpret_cast<unsigned long long *>(lds + cv.pS2);
@@ -1705,13 +1774,14 @@ __device__ __forceinline__ Ctx make_ctx(const ExtractParams &p, unsigned char *l
     }
 }
 
-// window (create_window, :278-296) -> LDS once as four shifted zero-padded fp32 copies, and its
-// support [j0, j1] (sh->j0 / j1) by ballots: every weight read is issued before the first use, so
-// the prologue costs one L2 round trip (windows longer than WPRE * NT loop over the rest).  Ends
-// with a barrier.
+// window (create_window, :278-296) -> LDS once as R4a's weight pairs (w_j^2, |w_j|) in fp32 from the
+// double window (dsp_device.h crop_plan), in two copies shifted by 0 / 1 entry -- so that the 8 pairs
+// of any step chunk are four aligned 16-B reads -- zero past L; and its support [j0, j1] (sh->j0 /
+// j1, for the ZCR) by ballots: every weight read is issued before the first use, so the prologue
+// costs one L2 round trip (windows longer than WPRE * NT loop over the rest).  Ends with a barrier.
 __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &c, int tid, int lane, int wid)
 {
-    float *wt = const_cast<float *>(c.wtab);  // 4 copies of wrow floats
+    float2 *wt = reinterpret_cast<float2 *>(const_cast<float *>(c.wtab));  // 2 copies of wrow pairs
     Shared *sh = c.sh;
     const int L = p.L;
     constexpr int WPRE = 3;
@@ -1726,17 +1796,18 @@ __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &
         sh->j1 = -1;
     }
     const int wrow = EXTRACT_WROW(L);
-    for (int t = tid; t < 4 * (wrow - L); t += NT) {  // zero pads: m < WPAD + r, m >= L + WPAD + r
-        const int r = t / (wrow - L), q = t - r * (wrow - L);
-        wt[r * wrow + (q < EXTRACT_WPAD + r ? q : q + L)] = 0.f;
+    for (int t = tid; t < 2 * (wrow - L); t += NT) {  // zero entries: copy h, m < h or m >= L + h
+        const int h = t / (wrow - L), q = t - h * (wrow - L);
+        wt[h * wrow + (q < h ? q : q + L)] = make_float2(0.f, 0.f);
     }
     __syncthreads();
     auto put_weight = [&](int q0, double w) {  // weight j = q0 + lane (q0 wave-uniform)
         const int j = q0 + lane;
         const bool in = j < L;
         if (in) {
-#pragma unroll
-            for (int r = 0; r < 4; r++) wt[r * wrow + j + EXTRACT_WPAD + r] = (float)w;
+            const float2 v = make_float2((float)(w * w), (float)fabs(w));
+            wt[j] = v;
+            wt[wrow + j + 1] = v;
         }
         const unsigned long long m = __ballot(in && w > 0.0);
         if (lane == 0 && m) {

@@ -32,13 +32,22 @@
 
 struct ExtractCarve {
     int sh, wtab, posw, wS2, wS1, vE, vZ, fE, fM, fZ, rank, pS2, pS1, ost, total;
+    int parts;  // R4's unit partials (dsp_device.h crop_plan), over wS2 / wS1 (dead by R4)
     int nvcap, fcap, nwmax;
 };
+
+// bytes of R4's unit partials for crops of up to fcap frames: 2 quantities x 16 floats per unit
+// and row group, units * NG <= max(CROP_SLOTS = 128, quads * NG) (dsp_device.h crop_plan)
+__host__ __device__ constexpr int extract_parts_bytes(int fcap, int L, int S)
+{
+    const int D = (L + S - 1) / S, NG = (D + 3) / 4, nq = (fcap + D - 1 + 3) / 4;
+    return 2 * 64 * (nq * NG > 128 ? nq * NG : 128);
+}
 
 // Region offsets from the capacities: nwmax 32-sample words (incl. the alignment lead), nvcap VAD
 // frames, fcap feature frames, wrow floats per shifted window copy.
 __host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvcap, int fcap, int wrow,
-                                                              bool rank = true)
+                                                              int parts_bytes, bool rank = true)
 {
     ExtractCarve c{};
     int o = 0;
@@ -51,10 +60,13 @@ __host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvc
     c.fcap = fcap;
     c.nwmax = nwmax;
     DSP_TAKE(sh, EXTRACT_SHARED_BYTES);
-    DSP_TAKE(wtab, 16 * wrow);                   // 4 zero-padded window copies, shifted by 0..3
+    DSP_TAKE(wtab, 16 * wrow);                   // 2 copies of (w^2, |w|) pairs, shifted by 0 / 1
     DSP_TAKE(posw, 4 * (c.nwmax + 2));           // positive-sample bits (+2 zero sentinels)
+    const int wsum0 = o;
     DSP_TAKE(wS2, 8 * c.nwmax);                  // per word: sum k^2 (exact, u64)
     DSP_TAKE(wS1, 4 * c.nwmax);                  // per word: sum k
+    c.parts = wsum0;
+    if (o < wsum0 + parts_bytes) o = (wsum0 + parts_bytes + 15) & ~15;
     DSP_TAKE(vE, 8 * c.nvcap);
     DSP_TAKE(vZ, 4 * c.nvcap);
     DSP_TAKE(fE, 4 * c.fcap);
@@ -75,7 +87,7 @@ __host__ __device__ inline ExtractCarve extract_carve(int ncap, int L, int S)
     const int nvcap = ncap >= L ? (ncap - L) / S + 1 : 0;
     const int fcap = ncap <= L ? 1 : (ncap - L + S - 1) / S + 1;
     const int nwmax = (ncap + 7 + 31) / 32 + 1;
-    return extract_carve_caps(nwmax, nvcap, fcap, EXTRACT_WROW(L));
+    return extract_carve_caps(nwmax, nvcap, fcap, EXTRACT_WROW(L), extract_parts_bytes(fcap, L, S));
 }
 
 // The fast kernel's layout is fixed at compile time (every LDS address an immediate) and serves
@@ -102,6 +114,7 @@ __host__ __device__ constexpr ExtractCarve extract_carve_fast()
     DSP_TAKE(sh, EXTRACT_SHARED_BYTES);
     DSP_TAKE(wtab, 16 * EXTRACT_FAST_WROW);
     DSP_TAKE(posw, 4 * (c.nwmax + 2));
+    c.parts = o;  // (extract_fast_fits: ceil(L / S) <= 8, so at most 16 KB: static_assert below)
     DSP_TAKE(wS2, 8 * c.nwmax);
     DSP_TAKE(wS1, 4 * c.nwmax);
     DSP_TAKE(vE, 8 * c.nvcap);
@@ -117,11 +130,15 @@ __host__ __device__ constexpr ExtractCarve extract_carve_fast()
 }
 static_assert(EXTRACT_WG_PER_CU * extract_carve_fast().total <= EXTRACT_LDS_LIMIT,
               "the FAST layout must fit EXTRACT_WG_PER_CU workgroups per CU");
+#define EXTRACT_FAST_DMAX 8  // ceil(L / S) of the FAST plan: crop partials of 128 frames fit wS2 / wS1
+static_assert(extract_carve_fast().vE - extract_carve_fast().parts >= 2 * 64 * 128,
+              "R4 partials over the FAST layout's word sums");
 __host__ __device__ inline bool extract_fast_fits(int ncap, int L, int S)
 {
     const ExtractCarve c = extract_carve(ncap, L, S);
     return (ncap + 7 + 31) / 32 <= EXTRACT_FAST_NWORD && c.nvcap <= EXTRACT_FAST_NV &&
-           c.fcap <= EXTRACT_FAST_NF && EXTRACT_WROW(L) <= EXTRACT_FAST_WROW;
+           c.fcap <= EXTRACT_FAST_NF && EXTRACT_WROW(L) <= EXTRACT_FAST_WROW &&
+           (L + S - 1) / S <= EXTRACT_FAST_DMAX;
 }
 
 #endif
