@@ -42,8 +42,9 @@
 #include "crop.h"
 
 #ifndef DSP_ABL  // the phase-ablation instrument (tools/ablate_build.sh, diagnostic builds only;
-#define DSP_ABL 0 // outputs are wrong): skip 1 = R4 frames, 2 = R5 jobs, 4 = R2 sign bits,
-#endif            // 8 = VAD pass-A partial moments -- the per-phase VALU budget of DESIGN.md §8
+#define DSP_ABL 0 // outputs are wrong): skip 1 = R4 ZCR, 2 = R5 jobs, 4 = R2 sign bits,
+#endif            // 8 = VAD pass-A partial moments, 16 = R4 MFMA chunks, 32 = R4 part trees -- the
+                  // per-phase VALU budget of DESIGN.md §8
 
 namespace dsp {
 
@@ -878,111 +879,6 @@ __device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur
 static constexpr int crop_frames(int m, int L, int S) { return (m <= L) ? 1 : (m - L + S - 1) / S + 1; }
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-// R4a: the unit partials of the crop (dsp_device.h crop_plan) -> parts.  Wave w takes units
-// 16 w + beta, beta = lane / 4 (one v_mfma_f32_4x4x1f32 block each, 16 per instruction); lane
-// (beta, l4 = lane % 4) supplies weight row 4 g + l4 and data column l4 (block 4 q + l4) of its unit
-// and ends holding that column's partials of the four rows.  A step is one sample per lane: its x^2
-// and |x| against (w^2, |w|), two MFMAs, alternating between two chains per quantity (even / odd
-// steps).  Steps come in chunks of 8: one 16-B load of the lane's 8 samples (the clip's own 2-byte
-// alignment, from L2) and four 16-B LDS reads of the 8 weight pairs.  Every lane runs the loop
-// (wave-uniform control flow around the MFMAs); lanes past the last unit compute unused partials.
-__device__ __forceinline__ void r4_units(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int L, int S,
-                                         int st, int en, const ClipStats &cs, const CropPlan &cp, int wid, int lane)
-{
-    const int units = cp.nq * cp.P;
-    const CanonX cx = canon_x(cs.mq, cs.t0);
-    const int beta = lane >> 2, l4 = lane & 3;
-    const __amdgpu_buffer_rsrc_t rs = clip_rsrc(p, cur);
-    const int n = cur.n, lead = cur.lead, wrow = EXTRACT_WROW(L);
-    // a 16-B load at an odd sample position drops its last dword when that dword straddles the
-    // clip's range end (range checks are per dword): when the clip ends on a vector boundary that
-    // dword holds the clip's last sample, patched in from an aligned load
-    const bool vfix = ((lead + n) & 7) == 0;
-    const int klast = vfix ? (int)(short)__builtin_amdgcn_raw_buffer_load_b16(rs, 2 * (lead + n - 1), 0, 0) : 0;
-    const float2 *wt = reinterpret_cast<const float2 *>(c.wtab);
-    for (int u0 = 16 * wid; u0 < units; u0 += 16 * NWAVE) {
-        const int u = u0 + beta;
-        const bool live = u < units;
-        const int q = live ? u / cp.P : 0, pp = live ? u - q * cp.P : 0;
-        const int t0 = pp * cp.T;
-        const int cs0 = st + (4 * q + l4) * S + t0;                      // clip sample of step 0
-        const int lim = live ? min(min(cp.T, S - t0), en - cs0) : cp.T;  // steps with data (then 0)
-        for (int g = 0; g < cp.NG; g++) {
-            const int j0 = (4 * g + l4) * S + t0;  // window index of step 0 (the lane's weight row)
-            f4v e0 = {0.f, 0.f, 0.f, 0.f}, e1 = e0, m0 = e0, m1 = e0;
-            short8 nxt = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rs, 2 * (lead + cs0), 0, 0));
-            for (int k = 0; k < cp.T; k += 8) {
-                const short8 raw = nxt;
-                if (k + 8 < cp.T)
-                    nxt = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rs, 2 * (lead + cs0 + k + 8), 0, 0));
-                // data: x of the lane's 8 samples, 0 past its steps (the part's end, the crop's end)
-                float2v xv[4];
-                const int rem = lim - k;
-                if (__builtin_expect(__ballot(rem < 8 || (vfix && rem == 8)) != 0, 0)) {
-                    const int cs = cs0 + k;
-                    short8 r = raw;
-                    if (vfix && ((lead + cs) & 1) && n - 1 >= cs && n - 1 < cs + 8) r[(n - 1 - cs) & 7] = (short)klast;
-#pragma unroll
-                    for (int h = 0; h < 4; h++) {
-                        xv[h] = canon_x2<false>(r[2 * h], r[2 * h + 1], cx);
-                        xv[h].x = 2 * h < rem ? xv[h].x : 0.f;
-                        xv[h].y = 2 * h + 1 < rem ? xv[h].y : 0.f;
-                    }
-                } else {
-#pragma unroll
-                    for (int h = 0; h < 4; h++) xv[h] = canon_x2<false>(raw[2 * h], raw[2 * h + 1], cx);
-                }
-                // weight pairs j .. j + 7, in two halves (zero past L; the copy shifted by j's
-                // parity is 16-B aligned)
-                const int jj = j0 + k;
-                const float4 *src = reinterpret_cast<const float4 *>(wt + (jj & 1) * wrow + jj + (jj & 1));
-#pragma unroll
-                for (int hh = 0; hh < 2; hh++) {
-                    float4 wa = {0.f, 0.f, 0.f, 0.f}, wb = wa;
-                    if (jj < L) {
-                        wa = src[2 * hh];
-                        wb = src[2 * hh + 1];
-                    }
-                    const float w2[4] = {wa.x, wa.z, wb.x, wb.z}, aw[4] = {wa.y, wa.w, wb.y, wb.w};
-                    float x2[4], ax[4];
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        const float2v xx = xv[2 * hh + h];
-                        const float2v sq = xx * xx;  // (no contraction: separate products)
-                        x2[2 * h] = sq.x;
-                        x2[2 * h + 1] = sq.y;
-                        ax[2 * h] = fabsf(xx.x);
-                        ax[2 * h + 1] = fabsf(xx.y);
-                    }
-#pragma unroll
-                    for (int s4 = 0; s4 < 4; s4++) {
-                        const int s = 4 * hh + s4;
-                        if (k + s < cp.T) {  // wave-uniform
-                            if (s & 1) {
-                                e1 = __builtin_amdgcn_mfma_f32_4x4x1f32(w2[s4], x2[s4], e1, 0, 0, 0);
-                                m1 = __builtin_amdgcn_mfma_f32_4x4x1f32(aw[s4], ax[s4], m1, 0, 0, 0);
-                            } else {
-                                e0 = __builtin_amdgcn_mfma_f32_4x4x1f32(w2[s4], x2[s4], e0, 0, 0, 0);
-                                m0 = __builtin_amdgcn_mfma_f32_4x4x1f32(aw[s4], ax[s4], m0, 0, 0, 0);
-                            }
-                        }
-                    }
-                }
-            }
-            if (live) {
-                f4v se, sm;
-                {
-#pragma clang fp contract(off)
-                    se = e0 + e1;
-                    sm = m0 + m1;
-                }
-                *reinterpret_cast<f4v *>(c.parts + crop_part_index(cp, 0, u, g, l4, 0)) = se;
-                *reinterpret_cast<f4v *>(c.parts + crop_part_index(cp, 1, u, g, l4, 0)) = sm;
-            }
-        }
-    }
-}
-
 // R4z: the ZCR of each frame of the crop (fe.py:34-40) -> c.fZ: one 16-lane row per frame, 4 per
 // wave.  A sample's sign survives windowing where w_j > 0 (j in [j0, j1]) and j < lim; transitions
 // into the window's zero ends / padding count too.
@@ -1002,6 +898,139 @@ __device__ __forceinline__ void r4_zcr(const Ctx &c, const ClipRef &cur, int L, 
             if (ib < fs + L - 1) z += pos_bit(c.posw, ib + lead);
         }
         if (act && rl == 0) c.fZ[g] = z;
+    }
+}
+
+#ifndef R4_QD
+#define R4_QD 2  // chunk loads in flight per lane (3 or 4: VGPR spills at 80)
+#endif
+// R4: the crop's frames.  E / M: the block sums of crop.h -> c.parts (R5 adds a frame's D of them);
+// the ZCR: r4_zcr -> c.fZ.  Wave w takes units 16 w + beta, beta = lane / 4 (one v_mfma_f32_4x4x1f32
+// block each, 16 per instruction; a quad's P units are the lanes 4 p + c of one 4P-lane group of a
+// wave); lane (beta, l4 = lane % 4) supplies weight row 4 g + l4 and data column l4 (block 4 q + l4)
+// of its unit and ends holding that column's partials of the four rows.  A step is one sample per
+// lane: its x^2 and |x| against (w^2, |w|), two MFMAs, alternating between two chains per quantity
+// (even / odd steps).  Steps come in chunks of 8: one 16-B load of the lane's 8 samples (the clip's
+// own 2-byte alignment, from L2 or beyond: the first four chunks are issued before the ZCR, the
+// rest four chunks ahead) and four 16-B LDS reads of the 8 weight pairs; a step past the lane's
+// part or the crop has data 0, which leaves the chains unchanged (fma(w, 0, c) = c), so a chunk
+// issues all its 8 steps and the MFMAs sit in straight-line code.  The partials go to LDS and the
+// wave that wrote a quad's P parts adds them (crop_tree16) into part 0's slot.  Lanes past the
+// last unit compute unused values.
+__device__ __forceinline__ void r4_crop(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int L, int S,
+                                        int st, int en, int F, const ClipStats &cs, const CropPlan &cp, int zj0,
+                                        int zj1, int wid, int lane)
+{
+    const int units = cp.nq * cp.P, lp = __builtin_ctz(cp.P);
+    const int beta = lane >> 2, l4 = lane & 3;
+    const __amdgpu_buffer_rsrc_t rs = clip_rsrc(p, cur);
+    const int n = cur.n, lead = cur.lead;
+    auto issue = [&](short8 (&qd)[R4_QD], int cs0, int k0) {
+#pragma unroll
+        for (int i = 0; i < R4_QD; i++)
+            if (k0 + 8 * i < cp.T)
+                qd[i] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rs, 2 * (lead + cs0 + k0 + 8 * i), 0, 0));
+    };
+    auto unit_cs0 = [&](int u0) {
+        const int u = u0 + beta, q = u >> lp, pp = u & (cp.P - 1);
+        return st + (4 * q + l4) * S + pp * cp.T;
+    };
+    short8 qd[R4_QD];
+    if (16 * wid < units) issue(qd, unit_cs0(16 * wid), 0);  // in flight across the ZCR
+    r4_zcr(c, cur, L, S, st, en, F, zj0, zj1, wid, lane);
+
+    const CanonX cx = canon_x(cs.mq, cs.t0);
+    const int wrow = EXTRACT_WROW(L);
+    // a 16-B load at an odd sample position drops its last dword when that dword straddles the
+    // clip's range end (range checks are per dword): when the clip ends on a vector boundary that
+    // dword holds the clip's last sample, patched in from an aligned load
+    const bool vfix = ((lead + n) & 7) == 0;
+    const int klast = vfix ? (int)(short)__builtin_amdgcn_raw_buffer_load_b16(rs, 2 * (lead + n - 1), 0, 0) : 0;
+    const float2 *wt = reinterpret_cast<const float2 *>(c.wtab);
+    const int wzero = (L + 1) & ~1;  // 8 zero pairs of copy 0 (16-B aligned): the weights past L
+    for (int u0 = 16 * wid; u0 < units; u0 += 16 * NWAVE) {
+        const int u = u0 + beta;
+        const bool live = u < units;
+        const int q = u >> lp, pp = u & (cp.P - 1);
+        const int t0 = pp * cp.T;
+        const int cs0 = unit_cs0(u0);                                    // clip sample of step 0
+        const int lim = live ? min(min(cp.T, S - t0), en - cs0) : cp.T;  // steps with data (then 0)
+        // a chunk at k needs masking when k > klim (fewer than 8 steps with data, or the vfix sample)
+        const int klim = lim - (vfix ? 9 : 8);
+        for (int g = 0; g < cp.NG; g++) {
+            if (u0 != 16 * wid || g > 0) issue(qd, cs0, 0);
+            const int j0 = (4 * g + l4) * S + t0;  // window index of step 0 (the lane's weight row)
+            const int wbase = (j0 & 1) * wrow + j0 + (j0 & 1);  // its pair in the copy of its parity
+            f4v e0 = {0.f, 0.f, 0.f, 0.f}, e1 = e0, m0 = e0, m1 = e0;
+            for (int k0 = 0; !(DSP_ABL & 16) && k0 < cp.T; k0 += 8 * R4_QD) {
+#pragma unroll
+                for (int i = 0; i < R4_QD; i++) {
+                    const int k = k0 + 8 * i;
+                    if (k < cp.T) {  // wave-uniform
+                        const short8 raw = qd[i];
+                        if (k + 8 * R4_QD < cp.T)
+                            qd[i] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rs, 2 * (lead + cs0 + k + 8 * R4_QD), 0, 0));
+                        // data: x of the lane's 8 samples, 0 past its steps (the part's end, the crop's end)
+                        float2v xv[4];
+                        const int rem = lim - k;
+                        if (__builtin_expect(__ballot(k > klim) != 0, 0)) {
+                            const int csk = cs0 + k;
+                            short8 r = raw;
+                            if (vfix && ((lead + csk) & 1) && n - 1 >= csk && n - 1 < csk + 8) r[(n - 1 - csk) & 7] = (short)klast;
+#pragma unroll
+                            for (int h = 0; h < 4; h++) {
+                                xv[h] = canon_x2<false>(r[2 * h], r[2 * h + 1], cx);
+                                xv[h].x = 2 * h < rem ? xv[h].x : 0.f;
+                                xv[h].y = 2 * h + 1 < rem ? xv[h].y : 0.f;
+                            }
+                        } else {
+#pragma unroll
+                            for (int h = 0; h < 4; h++) xv[h] = canon_x2<false>(raw[2 * h], raw[2 * h + 1], cx);
+                        }
+                        // weight pairs j .. j + 7 (zero past L; the copy shifted by j's parity is 16-B aligned)
+                        const float4 *src = reinterpret_cast<const float4 *>(wt + (j0 + k < L ? wbase + k : wzero));
+#pragma unroll
+                        for (int hh = 0; hh < 2; hh++) {
+                            const float4 wa = src[2 * hh], wb = src[2 * hh + 1];
+                            const float w2[4] = {wa.x, wa.z, wb.x, wb.z}, aw[4] = {wa.y, wa.w, wb.y, wb.w};
+#pragma unroll
+                            for (int h = 0; h < 2; h++) {
+                                const float2v xx = xv[2 * hh + h];
+                                const float2v sq = xx * xx;  // (no contraction: separate products)
+                                e0 = __builtin_amdgcn_mfma_f32_4x4x1f32(w2[2 * h], sq.x, e0, 0, 0, 0);
+                                m0 = __builtin_amdgcn_mfma_f32_4x4x1f32(aw[2 * h], fabsf(xx.x), m0, 0, 0, 0);
+                                e1 = __builtin_amdgcn_mfma_f32_4x4x1f32(w2[2 * h + 1], sq.y, e1, 0, 0, 0);
+                                m1 = __builtin_amdgcn_mfma_f32_4x4x1f32(aw[2 * h + 1], fabsf(xx.y), m1, 0, 0, 0);
+                            }
+                        }
+                    }
+                }
+            }
+            if (live) {
+                f4v se, sm;
+                {
+#pragma clang fp contract(off)
+                    se = e0 + e1;
+                    sm = m0 + m1;
+                }
+                *reinterpret_cast<f4v *>(c.parts + crop_part_index(cp, 0, u, g, l4, 0)) = se;
+                *reinterpret_cast<f4v *>(c.parts + crop_part_index(cp, 1, u, g, l4, 0)) = sm;
+            }
+            if (cp.P > 1 && !(DSP_ABL & 32)) {  // the wave's quads: B = the tree over the P parts, into part 0's slot
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const int nqw = 16 >> lp;  // quads of this wave
+                for (int t = lane; t < 32 * nqw; t += 64) {
+                    const int v = t & 3, col = (t >> 2) & 3, Q = (t >> 4) & 1, qq = (u0 >> lp) + (t >> 5);
+                    if (qq < cp.nq) {
+                        float *src = c.parts + crop_part_index(cp, Q, qq * cp.P, g, col, v);
+                        const int stride = cp.NG * 16;
+                        *src = crop_tree([&](int i) { return src[i * stride]; }, cp.P);
+                    }
+                }
+            }
+        }
     }
 }
 
@@ -1425,11 +1454,10 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     }
     STAMP(i, 4);
 
-    // ---- R4: windowed frames over the crop [st, en) (r4_units, r4_zcr) ------------------------
+    // ---- R4: windowed frames over the crop [st, en) (r4_crop) ------------------------------------
     const int F = crop_frames(en - st, L, S);
     const CropPlan cp = crop_plan(F, L, S);
-    r4_units(p, c, cur, L, S, st, en, cs, cp, wid, lane);
-    r4_zcr(c, cur, L, S, st, en, F, sh->j0, sh->j1, wid, lane);
+    r4_crop(p, c, cur, L, S, st, en, F, cs, cp, sh->j0, sh->j1, wid, lane);
     STAMP(i, 12);
     if constexpr (!EXACT)
         if (tid == 0) sh->next = resolve();  // claimed at the clip's start (-1: none)
@@ -1684,9 +1712,7 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     MARK(R4);
     const int F = crop_frames(en - st, L, S);
     const CropPlan cp = crop_plan(F, L, S);
-    r4_units(p, c, cur, L, S, st, en, cs, cp, wid, lane);
-    MARK(R4z);
-    r4_zcr(c, cur, L, S, st, en, F, sh->j0, sh->j1, wid, lane);
+    r4_crop(p, c, cur, L, S, st, en, F, cs, cp, sh->j0, sh->j1, wid, lane);
     STAMP(i, 12);
     __syncthreads();
     STAMP(i, 5);

@@ -32,12 +32,12 @@
 
 struct ExtractCarve {
     int sh, wtab, posw, wS2, wS1, vE, vZ, fE, fM, fZ, rank, pS2, pS1, ost, total;
-    int parts;  // R4's unit partials (dsp_device.h crop_plan), over wS2 / wS1 (dead by R4)
+    int parts;  // R4's unit partials and block sums (crop.h), over wS2 / wS1 (dead by R4)
     int nvcap, fcap, nwmax;
 };
 
-// bytes of R4's unit partials for crops of up to fcap frames: 2 quantities x 16 floats per unit
-// and row group, units * NG <= max(CROP_SLOTS = 128, quads * NG) (dsp_device.h crop_plan)
+// bytes of R4's unit partials (crop.h) for crops of up to fcap frames: 2 quantities x 16 floats per
+// unit and row group, units * NG <= max(128, quads * NG)
 __host__ __device__ constexpr int extract_parts_bytes(int fcap, int L, int S)
 {
     const int D = (L + S - 1) / S, NG = (D + 3) / 4, nq = (fcap + D - 1 + 3) / 4;
@@ -114,7 +114,7 @@ __host__ __device__ constexpr ExtractCarve extract_carve_fast()
     DSP_TAKE(sh, EXTRACT_SHARED_BYTES);
     DSP_TAKE(wtab, 16 * EXTRACT_FAST_WROW);
     DSP_TAKE(posw, 4 * (c.nwmax + 2));
-    c.parts = o;  // (extract_fast_fits: ceil(L / S) <= 8, so at most 16 KB: static_assert below)
+    c.parts = o;  // (extract_fast_fits: ceil(L / S) <= 8: static_assert below)
     DSP_TAKE(wS2, 8 * c.nwmax);
     DSP_TAKE(wS1, 4 * c.nwmax);
     DSP_TAKE(vE, 8 * c.nvcap);
@@ -130,8 +130,9 @@ __host__ __device__ constexpr ExtractCarve extract_carve_fast()
 }
 static_assert(EXTRACT_WG_PER_CU * extract_carve_fast().total <= EXTRACT_LDS_LIMIT,
               "the FAST layout must fit EXTRACT_WG_PER_CU workgroups per CU");
-#define EXTRACT_FAST_DMAX 8  // ceil(L / S) of the FAST plan: crop partials of 128 frames fit wS2 / wS1
-static_assert(extract_carve_fast().vE - extract_carve_fast().parts >= 2 * 64 * 128,
+#define EXTRACT_FAST_DMAX 8  // ceil(L / S) of the FAST plan: the partials of 128 frames fit wS2 / wS1
+static_assert(extract_carve_fast().vE - extract_carve_fast().parts >=
+                  extract_parts_bytes(EXTRACT_FAST_NF, EXTRACT_FAST_DMAX, 1),
               "R4 partials over the FAST layout's word sums");
 __host__ __device__ inline bool extract_fast_fits(int ncap, int L, int S)
 {

@@ -392,14 +392,13 @@ __device__ __forceinline__ void general_clip(const Params &p, Sh &s, const Ws &w
 
     // ---- windowed frames of the crop [st, en) (:378, :299-333; fe.py:12-43) ---------------
     // frame g covers crop samples [g S, g S + L), zero-padded past the crop.  E / M in the blocked-
-    // product order of dsp_device.h (crop_plan): the fused kernels compute each unit partial on
-    // the matrix cores (one v_mfma_f32_4x4x1f32 step = fmaf); here one lane computes a term's two
-    // chains in the same step order, so the bits are the fused kernels'.  One 16-lane row per
-    // frame: lane rl takes the terms (d, p) = rl, rl + 16, ... and the row adds them in order.
-    // The ZCR is exact either way.
+    // product order of crop.h: the fused kernels compute each unit partial on the matrix cores (one
+    // v_mfma_f32_4x4x1f32 step = fmaf); here, per row d of the frame, lane p of its 16-lane row
+    // computes part p's two chains in the same step order, the row forms B(g + d, d) by the same
+    // pairwise tree, and the frame adds the D block sums in order: the fused kernels' bits.  The ZCR
+    // is exact either way.
     const CanonX cx = canon_x(mq, t0);
     const CropPlan cp = crop_plan((int)F, L, S);
-    const int nterm = cp.D * cp.P;
     const int rl = lane & 15, row = lane >> 4;
     for (int64_t gi = wid; 4 * gi < F; gi += NWAVE) {
         const int64_t g = 4 * gi + row;
@@ -408,15 +407,14 @@ __device__ __forceinline__ void general_clip(const Params &p, Sh &s, const Ws &w
         const int64_t fs = st + gc * S;
         const int64_t lim = min((int64_t)L, en - fs);
         float es = 0.f, ms = 0.f;
-        for (int tq = 0; tq < nterm; tq += 16) {
+        for (int d = 0; d < cp.D; d++) {
             float te = 0.f, tm = 0.f;
-            if (tq + rl < nterm) {
-                const int d = (tq + rl) / cp.P, pp = tq + rl - d * cp.P;
-                const int tb = pp * cp.T, tp = min(cp.T, S - tb);
+            if (rl < cp.P) {
+                const int tb = rl * cp.T, tp = min(cp.T, S - tb);
                 float e0 = 0.f, e1 = 0.f, m0 = 0.f, m1 = 0.f;
                 for (int s2 = 0; s2 < tp; s2++) {
-                    const int j = d * S + tb + s2;         // window index
-                    const int64_t sj = fs + j;             // clip sample (crop block gc + d)
+                    const int j = d * S + tb + s2;  // window index
+                    const int64_t sj = fs + j;      // clip sample (crop block gc + d)
                     float w2 = 0.f, aw = 0.f, xs = 0.f;
                     if (j < L) {
                         const double wd = p.window[j];
@@ -440,10 +438,8 @@ __device__ __forceinline__ void general_clip(const Params &p, Sh &s, const Ws &w
                 te = e0 + e1;
                 tm = m0 + m1;
             }
-            for (int jx = 0; jx < 16 && tq + jx < nterm; jx++) {
-                es += __shfl(te, (lane & 48) + jx, 64);
-                ms += __shfl(tm, (lane & 48) + jx, 64);
-            }
+            es += crop_tree([&](int k) { return __shfl(te, (lane & 48) + k, 64); }, cp.P);
+            ms += crop_tree([&](int k) { return __shfl(tm, (lane & 48) + k, 64); }, cp.P);
         }
         int zc = 0;
         for (int j = rl; j + 1 < L; j += 16) {

@@ -5,6 +5,6 @@
 set -e
 cd "$(dirname "$0")/../dsp-audioreclabs_amd/csrc"
 n=$1; shift
-F="-O3 --offload-arch=gfx950 -std=c++17 -fPIC -I../../include -Wall -Wno-unused-function -mllvm -amdgpu-use-amdgpu-trackers=1"
+F="-O3 --offload-arch=gfx950 -std=c++17 -fPIC -I../../include -Wall -Wno-unused-function -mllvm -amdgpu-mfma-vgpr-form -mllvm -amdgpu-use-amdgpu-trackers=1"
 /opt/rocm/bin/hipcc $F "$@" -c extract.hip -o ../lib/obj/extract_$n.o
 /opt/rocm/bin/hipcc $F -shared ../lib/obj/extract_$n.o ../lib/obj/general.o ../lib/obj/knn.o ../lib/obj/wav_io.o -o ../lib/libdsp_audiorec_$n.so
