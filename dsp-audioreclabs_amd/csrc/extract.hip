@@ -39,12 +39,10 @@
 #include "dsp_audiorec.h"
 #include "extract_layout.h"
 #include "dsp_device.h"
-#include "crop.h"
 
 #ifndef DSP_ABL  // the phase-ablation instrument (tools/ablate_build.sh, diagnostic builds only;
-#define DSP_ABL 0 // outputs are wrong): skip 1 = R4 ZCR, 2 = R5 jobs, 4 = R2 sign bits,
-#endif            // 8 = VAD pass-A partial moments, 16 = R4 MFMA chunks, 32 = R4 part trees -- the
-                  // per-phase VALU budget of DESIGN.md §8
+#define DSP_ABL 0 // outputs are wrong): skip 1 = R4 frames, 2 = R5 jobs, 4 = R2 sign bits,
+#endif            // 8 = VAD pass-A partial moments -- the per-phase VALU budget of DESIGN.md §8
 
 namespace dsp {
 
@@ -187,7 +185,7 @@ __device__ __forceinline__ ClipRef clip_none()
 
 struct Ctx {
     Shared *sh;
-    const float *wtab;  // 2 copies of EXTRACT_WROW(L) (w^2, |w|) pairs, shifted by 0 / 1 (build_window)
+    const float *wtab;  // EXTRACT_WROW(L) floats per shifted copy r = 0..3 (extract_layout.h)
     uint32_t *posw;      // bit u of the buffer: sample u is real and positive after preprocess
     unsigned long long *wS2;
     int *wS1;
@@ -195,7 +193,8 @@ struct Ctx {
     int32_t *vZ;
     float *fE, *fM;
     int32_t *fZ;
-    float *parts;  // R4a's unit partials (crop_plan), over wS2 / wS1
+    uint16_t *zw;  // FAST: sign changes before word w within its 64-word segment (zseg_word)
+    int *ztot;     // FAST: sign changes of each 64-word segment, its last boundary left out
     int *rank;  // rank scratch: nvcap or 3 * fcap ints
     int *pS1;   // partial-word moments at the two ends of each VAD frame (2 * nvcap)
     unsigned long long *pS2;
@@ -730,6 +729,46 @@ __device__ __forceinline__ uint32_t pos_word(const short8 *q, int w, int nword, 
     return P;
 }
 
+// inclusive prefix sum over the wave's 64 lanes: row_shr 1 / 2 / 4 / 8 within each 16-lane row,
+// then row_bcast 15 / 31 carry the row totals upwards (every lane active)
+__device__ __forceinline__ int wave_incl_scan(int v)
+{
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+// FAST R2: the sign changes of buffer word w (pair 32 w + b <-> samples 32 w + b, + 1; bit 31 against
+// the next word's first sample, held by the next lane: one wave holds a 64-word segment of a
+// register row) counted and prefix-summed over the segment -> zw[w] (changes before w in the
+// segment) and ztot[seg] (the segment's changes without its last word's bit 31, which zseg_count
+// reads from posw).  Every lane active; P = 0 past the clip, as posw.
+__device__ __forceinline__ void zseg_word(const uint16_t *zw_, const int *zt_, uint32_t P, int w, int lane, int seg)
+{
+    uint16_t *zw = const_cast<uint16_t *>(zw_);
+    int *ztot = const_cast<int *>(zt_);
+    const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)P, 0x130, 0xF, 0xF, true);  // wave_shl:1
+    uint32_t ch = P ^ ((P >> 1) | (nb << 31));
+    if (lane == 63) ch &= 0x7fffffffu;
+    const int cz = __popc(ch), inc = wave_incl_scan(cz);
+    zw[w] = (uint16_t)(inc - cz);
+    if (lane == 63) ztot[seg] = inc;
+}
+// sign changes (set bits of chg_word) at buffer pairs [x0, x1) from the segment prefixes (FAST, after
+// the R2 barrier), for ranges of at most two segments (x1 - x0 <= 64 * 32)
+__device__ __forceinline__ int zseg_count(const uint32_t *posw, const uint16_t *zw, const int *ztot, int x0, int x1)
+{
+    if (x1 <= x0) return 0;
+    const int w0 = x0 >> 5, w1 = x1 >> 5, s0 = w0 >> 6;
+    int cnt = (int)zw[w1] - (int)zw[w0] - __popc(chg_word(posw, w0) & ((1u << (x0 & 31)) - 1u));
+    if (x1 & 31) cnt += __popc(chg_word(posw, w1) & ((1u << (x1 & 31)) - 1u));
+    if ((w1 >> 6) != s0) cnt += ztot[s0] + (int)(chg_word(posw, 64 * s0 + 63) >> 31);
+    return cnt;
+}
+
 // remove_dc / normalize_audio (:49-75) in sample units, computed redundantly by every thread from
 // the per-wave partial sums in sh->red_*: the reference's float64 mean of k/32768 is exact, so
 // m = fl(K/n) and the peak is max(fl(kmax - m), fl(m - kmin)); a sample is positive after
@@ -851,9 +890,8 @@ __device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur
             s1 += c.wS1[w];
             s2 += c.wS2[w];
         }
-        const int np_ = L - 1, ph = (np_ + 1) >> 1;  // pairs [u0, u1 - 1) in halves
-        const int x0 = u0 + min(lh * ph, np_), x1 = u0 + min((lh + 1) * ph, np_);
-        zc = chg_run(c.posw, x0, x1);
+        // sign changes at pairs [u0, u1 - 1) from R2's segment prefixes (lane 0 of the pair)
+        zc = lh ? 0 : zseg_count(c.posw, c.zw, c.ztot, u0, u1 - 1);
         // the partial word last: its load (issued before the R2 barrier) lands while the LDS
         // sums above run
         if (pa_w >= 0 && !(DSP_ABL & 8)) partial_moments(qa, pa_e0, pa_e1, s1, s2);
@@ -870,194 +908,128 @@ __device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur
     }
 }
 
-// R4: windowed frames over the crop [st, en) (:378, :299-333; fe.py:12-43).  E and M as the
-// blocked product of dsp_device.h (crop_plan: the crop's S-sample blocks against the window's
-// D = ceil(L / S) S-sample slices) on the matrix cores, the ZCR per frame from the positive bits.
-// (Rounds 2-6 summed each frame on its own: one 16-lane row per frame re-read the frame's 16-B
-// vectors from L2 and converted, centred and weighted every sample once per frame it lies in,
-// 2.5 times on average at 1102 / 441: ~7.5 VALU per sample pair and frame, 3.1k VALU per clip.)
-static constexpr int crop_frames(int m, int L, int S) { return (m <= L) ? 1 : (m - L + S - 1) / S + 1; }
-typedef float f4v __attribute__((ext_vector_type(4)));
-
-// R4z: the ZCR of each frame of the crop (fe.py:34-40) -> c.fZ: one 16-lane row per frame, 4 per
-// wave.  A sample's sign survives windowing where w_j > 0 (j in [j0, j1]) and j < lim; transitions
-// into the window's zero ends / padding count too.
-__device__ __forceinline__ void r4_zcr(const Ctx &c, const ClipRef &cur, int L, int S, int st, int en, int F, int j0,
-                                       int j1, int wrank, int lane)
+// R4: windowed frames over the crop [st, en) (:378, :299-333; fe.py:12-43) -> c.fE / fM / fZ.
+// One 16-lane row per frame (4 frames per wave), in the canonical order of dsp_device.h: the
+// frame's clip-relative 8-sample vectors are re-read from L2 (16-B loads at the clip's own 2-byte
+// alignment) and lane rl takes vectors va + rl + 16k, so the sums do not depend on where the clip
+// sits in the buffer and equal dsp_extract_general's.  Per sample y = w_j x (the reference's
+// windowed frame, :329-331), E += y^2, M += |y|; the weights of a vector's 8 samples are two
+// aligned 16-B reads from the window copy shifted by fs mod 4.  Returns F.
+// vectors per lane in one batch from L2: 7 (896 samples per row) leaves the FAST kernel without
+// VGPR spills; 9 (a whole 1102-sample frame) 2.71 ms, 7 2.65 ms, 6 / 8 2.61-2.64 / 2.66-2.68 ms at
+// 100k clips (profiles/r05s_ab_prefetch_kv.txt, r05kv_ab_r4_batch.txt)
+static constexpr int R4_KV = 7;
+template <bool ZSEG>  // ZCR from R2's segment prefixes (clip_fast) or by the row's lanes (clip_body)
+__device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int L, int S,
+                                         int st, int en, const ClipStats &cs, int j0, int j1, int wrank, int lane)
 {
-    const int lead = cur.lead;
+    const int n = cur.n, lead = cur.lead;
+    const int m = en - st;  // > 0 always (start < end)
+    const int F = (m <= L) ? 1 : (m - L + S - 1) / S + 1;
+    const float sE = cs.invMf * cs.invMf, sM = cs.invMf;
+    const int wrow = EXTRACT_WROW(L);
+    const CanonX cx = canon_x(cs.mq, cs.t0);
+    // a 16-B load ending past the clip's last buffer vector drops a dword that straddles the
+    // descriptor's end (range checks are per dword): with an odd lead and a clip ending on a
+    // vector boundary that dword holds the last sample, patched in from the aligned vector
+    const int vfix = ((lead & 1) && ((lead + n) & 7) == 0) ? (n - 1) >> 3 : -1;
+    const short klast = vfix >= 0 ? load_vec(p, cur, cur.nvec - 1)[7] : (short)0;
+    auto frame_vec = [&](auto padded_t, auto near_t, const short8 &x8, const float *wr, int jb, int lim,
+                         float2v &ea, float &m0, float &m1) {
+        constexpr bool PADDED = decltype(padded_t)::value, NEAR0 = decltype(near_t)::value;
+        const float4 wa = *reinterpret_cast<const float4 *>(wr + jb);
+        const float4 wb = *reinterpret_cast<const float4 *>(wr + jb + 4);
+        const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            float2v w = {wv[2 * h], wv[2 * h + 1]};
+            if (PADDED) {  // samples past the crop are zero padding
+                const int j = jb + 2 * h;  // window index of the pair's first sample
+                w.x = j < lim ? w.x : 0.f;
+                w.y = j + 1 < lim ? w.y : 0.f;
+            }
+            canon_pair(w, canon_x2<NEAR0>(x8[2 * h], x8[2 * h + 1], cx), ea, m0, m1);
+        }
+    };
+    constexpr int KV = R4_KV;
     const int rl = lane & 15, row = lane >> 4;
     for (int gi = wrank; !(DSP_ABL & 1) && 4 * gi < F; gi += NWAVE) {
         const int g = 4 * gi + row;
         const bool act = g < F;
-        const int fs = st + (act ? g : F - 1) * S;
+        const int gc = act ? g : F - 1;
+        const int fs = st + gc * S;
+        const int lim = min(L, en - fs);  // samples beyond the crop are zero padding
+        const bool padded = lim < L;
+        const int va = fs >> 3, vb = (fs + lim - 1) >> 3;
+        const int r = fs & 3;  // copy whose rows start at window index = -fs (mod 4)
+        const float *wr = c.wtab + r * wrow + EXTRACT_WPAD + r;  // wr[j] = w[j], j = -7 .. L + 7
+        float2v ea = {0.f, 0.f};
+        float m0 = 0.f, m1 = 0.f;
+        for (int v0 = va; v0 <= vb; v0 += 16 * KV) {
+            // the lane's vectors v0 + rl + 16k: one per-lane base (vl) and immediate offsets, a
+            // per-lane bound (vlim) against uniform 16k -- nine hoisted per-k indices spilled at
+            // 80 VGPRs and every reload waited for all of the batch's loads
+            const int vl = v0 + rl, vlim = vb - vl;
+            short8 xv[KV];
+#pragma unroll
+            for (int k = 0; k < KV; k++) xv[k] = load_cvec(p, cur, vl + 16 * k);
+            if (vfix >= 0)  // clip-uniform, rare
+#pragma unroll
+                for (int k = 0; k < KV; k++)
+                    if (vl + 16 * k == vfix) xv[k][(n - 1) & 7] = klast;
+            const int jl = 8 * vl - fs;  // window index of the lane's first vector
+            auto run = [&](auto pt, auto nt) {
+#pragma unroll
+                for (int k = 0; k < KV; k++)
+                    if (16 * k <= vlim) frame_vec(pt, nt, xv[k], wr, jl + 128 * k, lim, ea, m0, m1);
+            };
+            if (padded)
+                cx.near0 ? run(BoolT<true>(), BoolT<true>()) : run(BoolT<true>(), BoolT<false>());
+            else if (cx.near0)
+                run(BoolT<false>(), BoolT<true>());
+            else
+                run(BoolT<false>(), BoolT<false>());
+        }
+        const float E1 = dpp_row_reduce(ea.x + ea.y, OpAdd()) * sE;
+        const float M1 = dpp_row_reduce(m0 + m1, OpAdd()) * sM;
+        // ZCR of the windowed, padded frame: a sample's sign survives where w_j > 0 (j in
+        // [j0, j1]) and j < lim; transitions into the window's zero ends / padding count too
         const int ia = fs + j0, ib = min(fs + j1, en - 1);  // sample coords
-        int z = dpp_row_reduce(ia < ib ? chg_count(c.posw, ia + lead, ib + lead, rl, 16) : 0, OpAdd());
-        if (ia <= ib) {
-            if (j0 > 0) z += pos_bit(c.posw, ia + lead);
-            if (ib < fs + L - 1) z += pos_bit(c.posw, ib + lead);
-        }
-        if (act && rl == 0) c.fZ[g] = z;
-    }
-}
-
-#ifndef R4_QD
-#define R4_QD 2  // chunk loads in flight per lane (3 or 4: VGPR spills at 80)
-#endif
-// R4: the crop's frames.  E / M: the block sums of crop.h -> c.parts (R5 adds a frame's D of them);
-// the ZCR: r4_zcr -> c.fZ.  Wave w takes units 16 w + beta, beta = lane / 4 (one v_mfma_f32_4x4x1f32
-// block each, 16 per instruction; a quad's P units are the lanes 4 p + c of one 4P-lane group of a
-// wave); lane (beta, l4 = lane % 4) supplies weight row 4 g + l4 and data column l4 (block 4 q + l4)
-// of its unit and ends holding that column's partials of the four rows.  A step is one sample per
-// lane: its x^2 and |x| against (w^2, |w|), two MFMAs, alternating between two chains per quantity
-// (even / odd steps).  Steps come in chunks of 8: one 16-B load of the lane's 8 samples (the clip's
-// own 2-byte alignment, from L2 or beyond: the first four chunks are issued before the ZCR, the
-// rest four chunks ahead) and four 16-B LDS reads of the 8 weight pairs; a step past the lane's
-// part or the crop has data 0, which leaves the chains unchanged (fma(w, 0, c) = c), so a chunk
-// issues all its 8 steps and the MFMAs sit in straight-line code.  The partials go to LDS and the
-// wave that wrote a quad's P parts adds them (crop_tree16) into part 0's slot.  Lanes past the
-// last unit compute unused values.
-__device__ __forceinline__ void r4_crop(const ExtractParams &p, const Ctx &c, const ClipRef &cur, int L, int S,
-                                        int st, int en, int F, const ClipStats &cs, const CropPlan &cp, int zj0,
-                                        int zj1, int wid, int lane)
-{
-    const int units = cp.nq * cp.P, lp = __builtin_ctz(cp.P);
-    const int beta = lane >> 2, l4 = lane & 3;
-    const __amdgpu_buffer_rsrc_t rs = clip_rsrc(p, cur);
-    const int n = cur.n, lead = cur.lead;
-    auto issue = [&](short8 (&qd)[R4_QD], int cs0, int k0) {
-#pragma unroll
-        for (int i = 0; i < R4_QD; i++)
-            if (k0 + 8 * i < cp.T)
-                qd[i] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rs, 2 * (lead + cs0 + k0 + 8 * i), 0, 0));
-    };
-    auto unit_cs0 = [&](int u0) {
-        const int u = u0 + beta, q = u >> lp, pp = u & (cp.P - 1);
-        return st + (4 * q + l4) * S + pp * cp.T;
-    };
-    short8 qd[R4_QD];
-    if (16 * wid < units) issue(qd, unit_cs0(16 * wid), 0);  // in flight across the ZCR
-    r4_zcr(c, cur, L, S, st, en, F, zj0, zj1, wid, lane);
-
-    const CanonX cx = canon_x(cs.mq, cs.t0);
-    const int wrow = EXTRACT_WROW(L);
-    // a 16-B load at an odd sample position drops its last dword when that dword straddles the
-    // clip's range end (range checks are per dword): when the clip ends on a vector boundary that
-    // dword holds the clip's last sample, patched in from an aligned load
-    const bool vfix = ((lead + n) & 7) == 0;
-    const int klast = vfix ? (int)(short)__builtin_amdgcn_raw_buffer_load_b16(rs, 2 * (lead + n - 1), 0, 0) : 0;
-    const float2 *wt = reinterpret_cast<const float2 *>(c.wtab);
-    const int wzero = (L + 1) & ~1;  // 8 zero pairs of copy 0 (16-B aligned): the weights past L
-    for (int u0 = 16 * wid; u0 < units; u0 += 16 * NWAVE) {
-        const int u = u0 + beta;
-        const bool live = u < units;
-        const int q = u >> lp, pp = u & (cp.P - 1);
-        const int t0 = pp * cp.T;
-        const int cs0 = unit_cs0(u0);                                    // clip sample of step 0
-        const int lim = live ? min(min(cp.T, S - t0), en - cs0) : cp.T;  // steps with data (then 0)
-        // a chunk at k needs masking when k > klim (fewer than 8 steps with data, or the vfix sample)
-        const int klim = lim - (vfix ? 9 : 8);
-        for (int g = 0; g < cp.NG; g++) {
-            if (u0 != 16 * wid || g > 0) issue(qd, cs0, 0);
-            const int j0 = (4 * g + l4) * S + t0;  // window index of step 0 (the lane's weight row)
-            const int wbase = (j0 & 1) * wrow + j0 + (j0 & 1);  // its pair in the copy of its parity
-            f4v e0 = {0.f, 0.f, 0.f, 0.f}, e1 = e0, m0 = e0, m1 = e0;
-            for (int k0 = 0; !(DSP_ABL & 16) && k0 < cp.T; k0 += 8 * R4_QD) {
-#pragma unroll
-                for (int i = 0; i < R4_QD; i++) {
-                    const int k = k0 + 8 * i;
-                    if (k < cp.T) {  // wave-uniform
-                        const short8 raw = qd[i];
-                        if (k + 8 * R4_QD < cp.T)
-                            qd[i] = __builtin_bit_cast(short8, __builtin_amdgcn_raw_buffer_load_b128(rs, 2 * (lead + cs0 + k + 8 * R4_QD), 0, 0));
-                        // data: x of the lane's 8 samples, 0 past its steps (the part's end, the crop's end)
-                        float2v xv[4];
-                        const int rem = lim - k;
-                        if (__builtin_expect(__ballot(k > klim) != 0, 0)) {
-                            const int csk = cs0 + k;
-                            short8 r = raw;
-                            if (vfix && ((lead + csk) & 1) && n - 1 >= csk && n - 1 < csk + 8) r[(n - 1 - csk) & 7] = (short)klast;
-#pragma unroll
-                            for (int h = 0; h < 4; h++) {
-                                xv[h] = canon_x2<false>(r[2 * h], r[2 * h + 1], cx);
-                                xv[h].x = 2 * h < rem ? xv[h].x : 0.f;
-                                xv[h].y = 2 * h + 1 < rem ? xv[h].y : 0.f;
-                            }
-                        } else {
-#pragma unroll
-                            for (int h = 0; h < 4; h++) xv[h] = canon_x2<false>(raw[2 * h], raw[2 * h + 1], cx);
-                        }
-                        // weight pairs j .. j + 7 (zero past L; the copy shifted by j's parity is 16-B aligned)
-                        const float4 *src = reinterpret_cast<const float4 *>(wt + (j0 + k < L ? wbase + k : wzero));
-#pragma unroll
-                        for (int hh = 0; hh < 2; hh++) {
-                            const float4 wa = src[2 * hh], wb = src[2 * hh + 1];
-                            const float w2[4] = {wa.x, wa.z, wb.x, wb.z}, aw[4] = {wa.y, wa.w, wb.y, wb.w};
-#pragma unroll
-                            for (int h = 0; h < 2; h++) {
-                                const float2v xx = xv[2 * hh + h];
-                                const float2v sq = xx * xx;  // (no contraction: separate products)
-                                e0 = __builtin_amdgcn_mfma_f32_4x4x1f32(w2[2 * h], sq.x, e0, 0, 0, 0);
-                                m0 = __builtin_amdgcn_mfma_f32_4x4x1f32(aw[2 * h], fabsf(xx.x), m0, 0, 0, 0);
-                                e1 = __builtin_amdgcn_mfma_f32_4x4x1f32(w2[2 * h + 1], sq.y, e1, 0, 0, 0);
-                                m1 = __builtin_amdgcn_mfma_f32_4x4x1f32(aw[2 * h + 1], fabsf(xx.y), m1, 0, 0, 0);
-                            }
-                        }
-                    }
-                }
+        int z = 0;
+        if constexpr (ZSEG) {  // one lane per frame
+            if (rl == 0 && ia <= ib) {
+                z = zseg_count(c.posw, c.zw, c.ztot, ia + lead, ib + lead);
+                if (j0 > 0) z += pos_bit(c.posw, ia + lead);
+                if (ib < fs + L - 1) z += pos_bit(c.posw, ib + lead);
             }
-            if (live) {
-                f4v se, sm;
-                {
-#pragma clang fp contract(off)
-                    se = e0 + e1;
-                    sm = m0 + m1;
-                }
-                *reinterpret_cast<f4v *>(c.parts + crop_part_index(cp, 0, u, g, l4, 0)) = se;
-                *reinterpret_cast<f4v *>(c.parts + crop_part_index(cp, 1, u, g, l4, 0)) = sm;
-            }
-            if (cp.P > 1 && !(DSP_ABL & 32)) {  // the wave's quads: B = the tree over the P parts, into part 0's slot
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const int nqw = 16 >> lp;  // quads of this wave
-                for (int t = lane; t < 32 * nqw; t += 64) {
-                    const int v = t & 3, col = (t >> 2) & 3, Q = (t >> 4) & 1, qq = (u0 >> lp) + (t >> 5);
-                    if (qq < cp.nq) {
-                        float *src = c.parts + crop_part_index(cp, Q, qq * cp.P, g, col, v);
-                        const int stride = cp.NG * 16;
-                        *src = crop_tree([&](int i) { return src[i * stride]; }, cp.P);
-                    }
-                }
+        } else {
+            z = dpp_row_reduce(ia < ib ? chg_count(c.posw, ia + lead, ib + lead, rl, 16) : 0, OpAdd());
+            if (ia <= ib) {
+                if (j0 > 0) z += pos_bit(c.posw, ia + lead);
+                if (ib < fs + L - 1) z += pos_bit(c.posw, ib + lead);
             }
         }
+        if (act && rl == 0) {
+            c.fE[g] = E1;
+            c.fM[g] = M1;
+            c.fZ[g] = z;
+        }
     }
+    return F;
 }
 
 // R5 for F <= 128 (compute_statistics x 3, fe.py:46-62): six jobs on waves 0..5 -- wave q (q < 3)
 // the median of sequence q (E, M, ZCR) by an in-wave bitonic sort, wave 3 + q its mean /
 // population std (fp64 sums) / max / min -- no barrier.  np.median: the middle order statistic
 // (odd F) or the mean of the two middle ones.
-// E / M of frame j come from R4a's unit partials (crop_frame_sum, times invMf^2 / invMf); with
-// `keep` (the per-frame sequence is an output) the statistics waves also store them to c.fE / fM.
-__device__ __forceinline__ void r5_fast(const Ctx &c, int F, const CropPlan &cp, float invMf, bool keep,
-                                        float *featb, int wid, int lane)
+__device__ __forceinline__ void r5_fast(const Ctx &c, int F, float *featb, int wid, int lane)
 {
     const int r0 = (F - 1) / 2, r1 = F / 2;
-    const float sE = invMf * invMf, sM = invMf;
     for (int job = wid; !(DSP_ABL & 2) && job < 6; job += NWAVE) {
         const int q = job % 3;
-        auto get = [&](int j) -> float {
-            return q == 0 ? crop_frame_sum(c.parts, cp, j, 0) * sE
-                          : q == 1 ? crop_frame_sum(c.parts, cp, j, 1) * sM : (float)c.fZ[j];
-        };
+        auto get = [&](int j) -> float { return q == 0 ? c.fE[j] : q == 1 ? c.fM[j] : (float)c.fZ[j]; };
         const bool in0 = lane < F, in1 = lane + 64 < F;
         const float x0 = in0 ? get(lane) : 0.f, x1 = in1 ? get(lane + 64) : 0.f;
-        if (keep && job >= 3 && q < 2) {
-            float *dst = q == 0 ? c.fE : c.fM;
-            if (in0) dst[lane] = x0;
-            if (in1) dst[lane + 64] = x1;
-        }
         if (job < 3) {  // median by an in-wave bitonic sort
             unsigned a[2] = {in0 ? fkey(x0) : ~0u, in1 ? fkey(x1) : ~0u};
             float v0, v1;
@@ -1454,23 +1426,14 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     }
     STAMP(i, 4);
 
-    // ---- R4: windowed frames over the crop [st, en) (r4_crop) ------------------------------------
-    const int F = crop_frames(en - st, L, S);
-    const CropPlan cp = crop_plan(F, L, S);
-    r4_crop(p, c, cur, L, S, st, en, F, cs, cp, sh->j0, sh->j1, wid, lane);
+    // ---- R4: windowed frames over the crop [st, en) (r4_frames) --------------------------------
+    const int F = r4_frames<false>(p, c, cur, L, S, st, en, cs, sh->j0, sh->j1, wid, lane);
     STAMP(i, 12);
+    if (!FAST && F > 128)
+        for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
     if constexpr (!EXACT)
         if (tid == 0) sh->next = resolve();  // claimed at the clip's start (-1: none)
     __syncthreads();
-    if (!FAST && F > 128) {  // long sequences: E / M materialised for the rank passes
-        const float sE = cs.invMf * cs.invMf, sM = cs.invMf;
-        for (int t = tid; t < F; t += NT) {
-            c.fE[t] = crop_frame_sum(c.parts, cp, t, 0) * sE;
-            c.fM[t] = crop_frame_sum(c.parts, cp, t, 1) * sM;
-        }
-        for (int t = tid; t < 3 * F; t += NT) c.rank[t] = 0;
-        __syncthreads();
-    }
     if constexpr (!EXACT) {
         // regs are dead since R2: the next clip's words load while R5 runs (unconditional, a
         // clip_none() reads zeros, so the compiler's vmcnt bookkeeping stays exact)
@@ -1484,7 +1447,7 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
     const int r0 = (F - 1) / 2, r1 = F / 2;
     {
         if (FAST || F <= 128) {
-            r5_fast(c, F, cp, cs.invMf, p.seq != nullptr, featb, wid, lane);
+            r5_fast(c, F, featb, wid, lane);
         } else {  // long sequences: partial ranks over all waves, then one wave per sequence
             rank_partial([&](int q, int j) { return q == 2 ? (float)c.fZ[j] : (q == 0 ? c.fE[j] : c.fM[j]); },
                          3, F, c.rank, wid, lane);
@@ -1530,15 +1493,13 @@ __device__ __forceinline__ bool clip_body(const ExtractParams &p, const Ctx &c, 
         }
     }
     STAMP(i, 9);
-    if (p.seq) {
-        __syncthreads();  // c.fE / fM of r5_fast's statistics waves
+    if (p.seq)
         for (int g = tid; g < F && g < p.ld_seq; g += NT) {
             float *o = p.seq + ((size_t)i * p.ld_seq + g) * 3;
             o[0] = c.fE[g];
             o[1] = c.fM[g];
             o[2] = (float)c.fZ[g];
         }
-    }
     if (tid == 0) {
         if constexpr (EXACT) {
             out_se(p, i)[0] = st;
@@ -1651,12 +1612,17 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     // synchronises.  Issued earlier, with the clip's words still live, it costs spills whose
     // reloads wait for it: at the end of R1 3.38 ms, before R2 3.18, after R2 2.82
     // (profiles/r05h_ab.txt, r05i_ab.txt)
+    uint32_t P[RREG];
 #pragma unroll
     for (int r = 0; r < RREG; r++) {
         const int w = r * NT + tid;
-        if (w < nword) c.posw[w] = (DSP_ABL & 4) ? 0u : pos_word(&regs[4 * r], w, nword, lead, n, cs.tpos);
+        P[r] = (w < nword && !(DSP_ABL & 4)) ? pos_word(&regs[4 * r], w, nword, lead, n, cs.tpos) : 0u;
+        if (w < nword) c.posw[w] = P[r];
     }
+#pragma unroll
+    for (int r = 0; r < RREG; r++) zseg_word(c.zw, c.ztot, P[r], r * NT + tid, lane, r * NWAVE + wid);
     if (tid < 2) c.posw[nword + tid] = 0;
+    if (tid == 0) c.zw[RREG * NT] = 0;  // (a range ending at the last register word's end)
     MARK(paissue);
     short8 qa[4];
     int pa_e0 = 0, pa_e1 = 0, pa_w = -1;
@@ -1710,17 +1676,14 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
 
     // ---- R4: windowed frames over the crop [st, en) (r4_frames) --------------------------------
     MARK(R4);
-    const int F = crop_frames(en - st, L, S);
-    const CropPlan cp = crop_plan(F, L, S);
-    r4_crop(p, c, cur, L, S, st, en, F, cs, cp, sh->j0, sh->j1, wid, lane);
+    const int F = r4_frames<true>(p, c, cur, L, S, st, en, cs, sh->j0, sh->j1, wid, lane);
     STAMP(i, 12);
     __syncthreads();
     STAMP(i, 5);
 
     // ---- R5: 15-d statistics (compute_statistics x 3, fe.py:46-62) ------------------------
     MARK(R5);
-    const ExtractParams &qs = p;
-    r5_fast(c, F, cp, cs.invMf, qs.seq != nullptr, featb, wid, lane);
+    r5_fast(c, F, featb, wid, lane);
     if (wid == NWAVE - 1) {
         // idle in R5: the next clip's offsets to LDS, so that the loop top does not wait for a global
         // load (nor, through the in-order vmcnt, for the flushed output stores before it)
@@ -1730,15 +1693,14 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     }
     STAMP(i, 9);
     MARK(tail);
-    if (qs.seq) {
-        __syncthreads();  // c.fE / fM of r5_fast's statistics waves
+    const ExtractParams &qs = p;
+    if (qs.seq)
         for (int g = tid; g < F && g < qs.ld_seq; g += NT) {
             float *o = qs.seq + ((size_t)i * qs.ld_seq + g) * 3;
             o[0] = c.fE[g];
             o[1] = c.fM[g];
             o[2] = (float)c.fZ[g];
         }
-    }
     if (tid == 0) {
         int32_t *orow = c.orow + DSP_OUT_ROW_WORDS * oslot;
         orow[15] = st;
@@ -1780,8 +1742,9 @@ __device__ __forceinline__ Ctx ctx_from(const ExtractCarve &cv, unsigned char *l
     c.fE = reinterpret_cast<float *>(lds + cv.fE);
     c.fM = reinterpret_cast<float *>(lds + cv.fM);
     c.fZ = reinterpret_cast<int32_t *>(lds + cv.fZ);
-    c.parts = reinterpret_cast<float *>(lds + cv.parts);
     c.rank = reinterpret_cast<int *>(lds + cv.rank);
+    c.zw = reinterpret_cast<uint16_t *>(lds + cv.zw);
+    c.ztot = reinterpret_cast<int *>(lds + cv.ztot);
     c.pS1 = reinterpret_cast<int *>(lds + cv.pS1);
     c.pS2 = reinterpret_cast<unsigned long long *>(lds + cv.pS2);
     c.orow = reinterpret_cast<int32_t *>(lds + cv.ost);
@@ -1800,14 +1763,13 @@ __device__ __forceinline__ Ctx make_ctx(const ExtractParams &p, unsigned char *l
     }
 }
 
-// window (create_window, :278-296) -> LDS once as R4a's weight pairs (w_j^2, |w_j|) in fp32 from the
-// double window (dsp_device.h crop_plan), in two copies shifted by 0 / 1 entry -- so that the 8 pairs
-// of any step chunk are four aligned 16-B reads -- zero past L; and its support [j0, j1] (sh->j0 /
-// j1, for the ZCR) by ballots: every weight read is issued before the first use, so the prologue
-// costs one L2 round trip (windows longer than WPRE * NT loop over the rest).  Ends with a barrier.
+// window (create_window, :278-296) -> LDS once as four shifted zero-padded fp32 copies, and its
+// support [j0, j1] (sh->j0 / j1) by ballots: every weight read is issued before the first use, so
+// the prologue costs one L2 round trip (windows longer than WPRE * NT loop over the rest).  Ends
+// with a barrier.
 __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &c, int tid, int lane, int wid)
 {
-    float2 *wt = reinterpret_cast<float2 *>(const_cast<float *>(c.wtab));  // 2 copies of wrow pairs
+    float *wt = const_cast<float *>(c.wtab);  // 4 copies of wrow floats
     Shared *sh = c.sh;
     const int L = p.L;
     constexpr int WPRE = 3;
@@ -1822,18 +1784,17 @@ __device__ __forceinline__ void build_window(const ExtractParams &p, const Ctx &
         sh->j1 = -1;
     }
     const int wrow = EXTRACT_WROW(L);
-    for (int t = tid; t < 2 * (wrow - L); t += NT) {  // zero entries: copy h, m < h or m >= L + h
-        const int h = t / (wrow - L), q = t - h * (wrow - L);
-        wt[h * wrow + (q < h ? q : q + L)] = make_float2(0.f, 0.f);
+    for (int t = tid; t < 4 * (wrow - L); t += NT) {  // zero pads: m < WPAD + r, m >= L + WPAD + r
+        const int r = t / (wrow - L), q = t - r * (wrow - L);
+        wt[r * wrow + (q < EXTRACT_WPAD + r ? q : q + L)] = 0.f;
     }
     __syncthreads();
     auto put_weight = [&](int q0, double w) {  // weight j = q0 + lane (q0 wave-uniform)
         const int j = q0 + lane;
         const bool in = j < L;
         if (in) {
-            const float2 v = make_float2((float)(w * w), (float)fabs(w));
-            wt[j] = v;
-            wt[wrow + j + 1] = v;
+#pragma unroll
+            for (int r = 0; r < 4; r++) wt[r * wrow + j + EXTRACT_WPAD + r] = (float)w;
         }
         const unsigned long long m = __ballot(in && w > 0.0);
         if (lane == 0 && m) {

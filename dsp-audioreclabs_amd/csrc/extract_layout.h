@@ -32,22 +32,14 @@
 
 struct ExtractCarve {
     int sh, wtab, posw, wS2, wS1, vE, vZ, fE, fM, fZ, rank, pS2, pS1, ost, total;
-    int parts;  // R4's unit partials and block sums (crop.h), over wS2 / wS1 (dead by R4)
+    int zw, ztot;  // FAST: sign-change counts, prefix within 64-word segments (u16) and segment totals
     int nvcap, fcap, nwmax;
 };
-
-// bytes of R4's unit partials (crop.h) for crops of up to fcap frames: 2 quantities x 16 floats per
-// unit and row group, units * NG <= max(128, quads * NG)
-__host__ __device__ constexpr int extract_parts_bytes(int fcap, int L, int S)
-{
-    const int D = (L + S - 1) / S, NG = (D + 3) / 4, nq = (fcap + D - 1 + 3) / 4;
-    return 2 * 64 * (nq * NG > 128 ? nq * NG : 128);
-}
 
 // Region offsets from the capacities: nwmax 32-sample words (incl. the alignment lead), nvcap VAD
 // frames, fcap feature frames, wrow floats per shifted window copy.
 __host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvcap, int fcap, int wrow,
-                                                              int parts_bytes, bool rank = true)
+                                                              bool rank = true)
 {
     ExtractCarve c{};
     int o = 0;
@@ -60,13 +52,10 @@ __host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvc
     c.fcap = fcap;
     c.nwmax = nwmax;
     DSP_TAKE(sh, EXTRACT_SHARED_BYTES);
-    DSP_TAKE(wtab, 16 * wrow);                   // 2 copies of (w^2, |w|) pairs, shifted by 0 / 1
+    DSP_TAKE(wtab, 16 * wrow);                   // 4 zero-padded window copies, shifted by 0..3
     DSP_TAKE(posw, 4 * (c.nwmax + 2));           // positive-sample bits (+2 zero sentinels)
-    const int wsum0 = o;
     DSP_TAKE(wS2, 8 * c.nwmax);                  // per word: sum k^2 (exact, u64)
     DSP_TAKE(wS1, 4 * c.nwmax);                  // per word: sum k
-    c.parts = wsum0;
-    if (o < wsum0 + parts_bytes) o = (wsum0 + parts_bytes + 15) & ~15;
     DSP_TAKE(vE, 8 * c.nvcap);
     DSP_TAKE(vZ, 4 * c.nvcap);
     DSP_TAKE(fE, 4 * c.fcap);
@@ -76,6 +65,7 @@ __host__ __device__ constexpr ExtractCarve extract_carve_caps(int nwmax, int nvc
     DSP_TAKE(pS2, 16 * c.nvcap);  // partial-word moments at the two ends of each VAD frame
     DSP_TAKE(pS1, 8 * c.nvcap);
     DSP_TAKE(ost, 4 * 19 * EXTRACT_OSTAGE);  // staged outputs of one clip chunk (feat, start/end, frames, status)
+    c.zw = c.ztot = o;  // FAST layout only
 #undef DSP_TAKE
     c.total = o;
     return c;
@@ -87,7 +77,7 @@ __host__ __device__ inline ExtractCarve extract_carve(int ncap, int L, int S)
     const int nvcap = ncap >= L ? (ncap - L) / S + 1 : 0;
     const int fcap = ncap <= L ? 1 : (ncap - L + S - 1) / S + 1;
     const int nwmax = (ncap + 7 + 31) / 32 + 1;
-    return extract_carve_caps(nwmax, nvcap, fcap, EXTRACT_WROW(L), extract_parts_bytes(fcap, L, S));
+    return extract_carve_caps(nwmax, nvcap, fcap, EXTRACT_WROW(L));
 }
 
 // The fast kernel's layout is fixed at compile time (every LDS address an immediate) and serves
@@ -114,7 +104,6 @@ __host__ __device__ constexpr ExtractCarve extract_carve_fast()
     DSP_TAKE(sh, EXTRACT_SHARED_BYTES);
     DSP_TAKE(wtab, 16 * EXTRACT_FAST_WROW);
     DSP_TAKE(posw, 4 * (c.nwmax + 2));
-    c.parts = o;  // (extract_fast_fits: ceil(L / S) <= 8: static_assert below)
     DSP_TAKE(wS2, 8 * c.nwmax);
     DSP_TAKE(wS1, 4 * c.nwmax);
     DSP_TAKE(vE, 8 * c.nvcap);
@@ -123,6 +112,8 @@ __host__ __device__ constexpr ExtractCarve extract_carve_fast()
     DSP_TAKE(fM, 4 * c.fcap);
     DSP_TAKE(fZ, 4 * c.fcap);
     DSP_TAKE(ost, 4 * 19 * EXTRACT_OSTAGE);
+    DSP_TAKE(zw, 2 * (c.nwmax + 2));           // per word: sign changes before it in its 64-word segment
+    DSP_TAKE(ztot, 4 * (EXTRACT_FAST_NWORD / 64 + 1));  // per segment: its sign changes (last boundary excluded)
     c.rank = c.pS1 = c.pS2 = o;  // unused by the FAST layout (<= 128 frames; pass A sums in registers)
 #undef DSP_TAKE
     c.total = o;
@@ -130,16 +121,11 @@ __host__ __device__ constexpr ExtractCarve extract_carve_fast()
 }
 static_assert(EXTRACT_WG_PER_CU * extract_carve_fast().total <= EXTRACT_LDS_LIMIT,
               "the FAST layout must fit EXTRACT_WG_PER_CU workgroups per CU");
-#define EXTRACT_FAST_DMAX 8  // ceil(L / S) of the FAST plan: the partials of 128 frames fit wS2 / wS1
-static_assert(extract_carve_fast().vE - extract_carve_fast().parts >=
-                  extract_parts_bytes(EXTRACT_FAST_NF, EXTRACT_FAST_DMAX, 1),
-              "R4 partials over the FAST layout's word sums");
 __host__ __device__ inline bool extract_fast_fits(int ncap, int L, int S)
 {
     const ExtractCarve c = extract_carve(ncap, L, S);
     return (ncap + 7 + 31) / 32 <= EXTRACT_FAST_NWORD && c.nvcap <= EXTRACT_FAST_NV &&
-           c.fcap <= EXTRACT_FAST_NF && EXTRACT_WROW(L) <= EXTRACT_FAST_WROW &&
-           (L + S - 1) / S <= EXTRACT_FAST_DMAX;
+           c.fcap <= EXTRACT_FAST_NF && EXTRACT_WROW(L) <= EXTRACT_FAST_WROW;
 }
 
 #endif

@@ -22,7 +22,6 @@
 
 #include "dsp_audiorec.h"
 #include "dsp_device.h"
-#include "crop.h"
 
 namespace dsp {
 namespace gen {
@@ -391,56 +390,30 @@ __device__ __forceinline__ void general_clip(const Params &p, Sh &s, const Ws &w
     }
 
     // ---- windowed frames of the crop [st, en) (:378, :299-333; fe.py:12-43) ---------------
-    // frame g covers crop samples [g S, g S + L), zero-padded past the crop.  E / M in the blocked-
-    // product order of crop.h: the fused kernels compute each unit partial on the matrix cores (one
-    // v_mfma_f32_4x4x1f32 step = fmaf); here, per row d of the frame, lane p of its 16-lane row
-    // computes part p's two chains in the same step order, the row forms B(g + d, d) by the same
-    // pairwise tree, and the frame adds the D block sums in order: the fused kernels' bits.  The ZCR
-    // is exact either way.
+    // frame g covers crop samples [g S, g S + L), zero-padded past the crop.  One 16-lane row per
+    // frame, E / M in the canonical order of dsp_device.h (the fused kernel's, same bits); the
+    // ZCR is exact either way.
     const CanonX cx = canon_x(mq, t0);
-    const CropPlan cp = crop_plan((int)F, L, S);
     const int rl = lane & 15, row = lane >> 4;
     for (int64_t gi = wid; 4 * gi < F; gi += NWAVE) {
         const int64_t g = 4 * gi + row;
         const bool act = g < F;
-        const int64_t gc = act ? g : F - 1;
-        const int64_t fs = st + gc * S;
+        const int64_t fs = st + (act ? g : F - 1) * S;
         const int64_t lim = min((int64_t)L, en - fs);
-        float es = 0.f, ms = 0.f;
-        for (int d = 0; d < cp.D; d++) {
-            float te = 0.f, tm = 0.f;
-            if (rl < cp.P) {
-                const int tb = rl * cp.T, tp = min(cp.T, S - tb);
-                float e0 = 0.f, e1 = 0.f, m0 = 0.f, m1 = 0.f;
-                for (int s2 = 0; s2 < tp; s2++) {
-                    const int j = d * S + tb + s2;  // window index
-                    const int64_t sj = fs + j;      // clip sample (crop block gc + d)
-                    float w2 = 0.f, aw = 0.f, xs = 0.f;
-                    if (j < L) {
-                        const double wd = p.window[j];
-                        w2 = (float)(wd * wd);
-                        aw = (float)fabs(wd);
-                    }
-                    if (sj < en) xs = canon_xval(sample(x, sj), cx);
-                    float x2;
-                    {
-#pragma clang fp contract(off)
-                        x2 = xs * xs;
-                    }
-                    if (s2 & 1) {
-                        e1 = fmaf(w2, x2, e1);
-                        m1 = fmaf(aw, fabsf(xs), m1);
-                    } else {
-                        e0 = fmaf(w2, x2, e0);
-                        m0 = fmaf(aw, fabsf(xs), m0);
-                    }
+        const int64_t va = fs >> 3, vb = (fs + lim - 1) >> 3;
+        float2v ea = {0.f, 0.f};
+        float m0 = 0.f, m1 = 0.f;
+        for (int64_t v = va + rl; v <= vb; v += 16)
+            for (int h = 0; h < 4; h++) {
+                float2v wv, xv;
+                for (int t = 0; t < 2; t++) {
+                    const int64_t sj = 8 * v + 2 * h + t, j = sj - fs;
+                    wv[t] = (j >= 0 && j < lim) ? (float)p.window[j] : 0.f;
+                    xv[t] = sj < n ? canon_xval(sample(x, sj), cx) : 0.f;
                 }
-                te = e0 + e1;
-                tm = m0 + m1;
+                canon_pair(wv, xv, ea, m0, m1);
             }
-            es += crop_tree([&](int k) { return __shfl(te, (lane & 48) + k, 64); }, cp.P);
-            ms += crop_tree([&](int k) { return __shfl(tm, (lane & 48) + k, 64); }, cp.P);
-        }
+        const float es = dpp_row_reduce(ea.x + ea.y, OpAdd()), ms = dpp_row_reduce(m0 + m1, OpAdd());
         int zc = 0;
         for (int j = rl; j + 1 < L; j += 16) {
             const bool p0 = j < lim && p.window[j] > 0.0 && sample(x, fs + j) >= tpos;
