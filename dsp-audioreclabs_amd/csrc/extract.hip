@@ -1156,11 +1156,15 @@ __device__ __forceinline__ int queue_end(const ClipQueue &Q, Shared *sh, unsigne
     int y = sh->cy;
     for (;;) {
         const int D = Q.nch - Q.s0;  // the claimed chunks [s0, nch), in NR ranges
-        const unsigned c0 = (unsigned)(Q.s0 + y * D / NR), c1 = (unsigned)(Q.s0 + (y + 1) * D / NR);
-        if (c0 + ret < c1) {
-            const int first = (int)(c0 + ret) * Q.ch;
+        const int c0 = Q.s0 + y * D / NR, c1 = Q.s0 + (y + 1) * D / NR;
+        // the range's clips [r0, r1): chunks of ch, then its last ~2 clips per workgroup of an XCD
+        // one at a time, so that the workgroups run out of work together (guided tail)
+        const int r0 = c0 * Q.ch, r1 = min(Q.B, c1 * Q.ch);
+        const int nbig = max(0, r1 - r0 - 2 * ((int)gridDim.x / NR)) / Q.ch;
+        const int first = (int)ret < nbig ? r0 + (int)ret * Q.ch : r0 + nbig * Q.ch + ((int)ret - nbig);
+        if ((int)ret < nbig || first < r1) {
             sh->qnext = first + 1;
-            sh->qend = min(Q.B, first + Q.ch);
+            sh->qend = (int)ret < nbig ? first + Q.ch : first + 1;
             return first;
         }
         // this range is used up: the next one (a blocking claim, rare: the end of the launch)
