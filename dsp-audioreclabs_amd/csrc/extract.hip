@@ -672,8 +672,12 @@ __device__ __forceinline__ void r1_edges(int xv, int nword, int lane, R1Acc &a, 
     // operations execute in program order, so the zeroing lands first
     const int w = lane < 32 ? 0 : nword - 1;
     if ((lane & 31) == 0 && (lane == 0 || nword > 1)) {
-        wS1[w] = 0;
-        wS2[w] = 0;
+        // (zeros made here: a 64-bit zero kept live from the prologue was spilled to scratch)
+        int z1 = 0;
+        unsigned long long z2 = 0;
+        asm volatile("" : "+v"(z1), "+v"(z2));
+        wS1[w] = z1;
+        wS2[w] = z2;
     }
     if (valid) {
         __hip_atomic_fetch_add(wS1 + w, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1726,8 +1730,10 @@ __device__ __forceinline__ void write_bad_clip(const ExtractParams &p, int i, in
     if (tid == 0) {
         const int64_t nn = p.offsets[i + 1] - p.offsets[i];
         *out_st(p, i) = nn <= 0 ? DSP_CLIP_EMPTY : DSP_CLIP_TOO_LONG;
-        out_se(p, i)[0] = 0;
-        out_se(p, i)[1] = 0;
+        int z = 0;
+        asm volatile("" : "+v"(z));
+        out_se(p, i)[0] = z;
+        out_se(p, i)[1] = z;
         *out_nf(p, i) = 0;
     }
 }
