@@ -2093,12 +2093,15 @@ extern "C" int dsp_extract_features(const int16_t *pcm, const int64_t *offsets, 
     p.qchunk = 2 * B <= 3 * (int64_t)grid ? 0 : B <= 2 * (int64_t)grid ? 1 : B < 64 * (int64_t)grid ? 2 : 4;
     static_assert(EXTRACT_OSTAGE >= 4, "qchunk <= EXTRACT_OSTAGE");
     const hipStream_t s = (hipStream_t)stream;
+    // the near-tie redo: one workgroup per CU (near ties are rare; a launch without any returns at
+    // once, and dispatching a third of the main grid makes that empty launch shorter)
+    const int xgrid = std::min(grid, num_cus);
     if (fast) {
         hipLaunchKernelGGL(dsp::extract_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
-        hipLaunchKernelGGL(dsp::extract_exact_kernel<true>, dim3(grid), dim3(dsp::NT), lds_launch + 4 * dsp::NT, s, p);
+        hipLaunchKernelGGL(dsp::extract_exact_kernel<true>, dim3(xgrid), dim3(dsp::NT), lds_launch + 4 * dsp::NT, s, p);
     } else {
         hipLaunchKernelGGL(dsp::extract_kernel<false>, dim3(grid), dim3(dsp::NT), lds_launch, s, p);
-        hipLaunchKernelGGL(dsp::extract_exact_kernel<false>, dim3(grid), dim3(dsp::NT), lds_launch + 4 * dsp::NT, s, p);
+        hipLaunchKernelGGL(dsp::extract_exact_kernel<false>, dim3(xgrid), dim3(dsp::NT), lds_launch + 4 * dsp::NT, s, p);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? DSP_OK : DSP_ERR_HIP + (int)e;
