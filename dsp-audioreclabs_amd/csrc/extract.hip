@@ -533,6 +533,42 @@ __device__ __forceinline__ void partial_moments(const short8 (&q)[4], int e0, in
     t2 += s2;
 }
 
+// FAST pass A: partial_moments unrolled over the word's four vectors (no value selects) and with the
+// squares of two pairs chained in one 32-bit v_dot2 (as R1's interior words: 4 x 32768^2 = 2^32
+// wraps only when all four samples are -32768, so a clip holding a -32768 sample (kneg, clip-
+// uniform) adds every pair's squares to the 64-bit sum on its own)
+__device__ __forceinline__ void partial_moments_fast(const short8 (&q)[4], int e0, int e1, bool kneg, int &t1,
+                                                     unsigned long long &t2)
+{
+    const uint32_t hi = e1 >= 32 ? ~0u : (1u << e1) - 1u;
+    const uint32_t M = hi & ~((1u << e0) - 1u);  // e0 < 32
+    const short2v ones = {1, 1};
+    int s1 = 0;
+    unsigned long long s2 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t Mk = M >> (8 * k);
+        short2v dm[4];
+#pragma unroll
+        for (int h = 0; h < 4; h++) {  // pair 4k + h: elements 8k + 2h, 8k + 2h + 1
+            const uint32_t b0 = (uint32_t)__builtin_amdgcn_sbfe((int)Mk, 2 * h, 1);
+            const uint32_t b1 = (uint32_t)__builtin_amdgcn_sbfe((int)Mk, 2 * h + 1, 1);
+            const uint32_t m = (b0 & 0x0000FFFFu) | (b1 & 0xFFFF0000u);
+            dm[h] = __builtin_bit_cast(short2v, __builtin_bit_cast(uint32_t, half_pair(q[k], h)) & m);
+            s1 = __builtin_amdgcn_sdot2(dm[h], ones, s1, false);
+        }
+        if (kneg) {
+#pragma unroll
+            for (int h = 0; h < 4; h++) s2 += (unsigned)sq2(dm[h]);
+        } else {
+            s2 += (unsigned)sq2acc(dm[1], sq2(dm[0]));
+            s2 += (unsigned)sq2acc(dm[3], sq2(dm[2]));
+        }
+    }
+    t1 += s1;
+    t2 += s2;
+}
+
 // values every lane holds alike (read from LDS, say): pinned to scalar registers
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ float uni(float v)
@@ -898,7 +934,7 @@ __device__ __forceinline__ void vad_frames_fast(const Ctx &c, const ClipRef &cur
         zc = lh ? 0 : zseg_count(c.posw, c.zw, c.ztot, u0, u1 - 1);
         // the partial word last: its load (issued before the R2 barrier) lands while the LDS
         // sums above run
-        if (pa_w >= 0 && !(DSP_ABL & 8)) partial_moments(qa, pa_e0, pa_e1, s1, s2);
+        if (pa_w >= 0 && !(DSP_ABL & 8)) partial_moments_fast(qa, pa_e0, pa_e1, cs.kneg, s1, s2);
     }
     s1 += dpp_i(s1, DPP_QXOR1);
     {
