@@ -42,7 +42,8 @@
 
 #ifndef DSP_ABL  // the phase-ablation instrument (tools/ablate_build.sh, diagnostic builds only;
 #define DSP_ABL 0 // outputs are wrong): skip 1 = R4 frames, 2 = R5 jobs, 4 = R2 sign bits,
-#endif            // 8 = VAD pass-A partial moments -- the per-phase VALU budget of DESIGN.md §8
+#endif            // 8 = VAD pass-A partial moments, 64 = p90 selection -- the per-phase VALU budget of
+                  // DESIGN.md §8
 
 namespace dsp {
 
@@ -841,9 +842,10 @@ __device__ __forceinline__ ClipStats clip_stats(const Shared *sh, int n, int L, 
     return s;
 }
 
-// p90 order statistics of the VAD energies (:198) by ONE wave, nv <= 128: bitonic sort of the high
-// halves of the order-preserving keys; the rank's element is the one holding that high half, or,
-// when several do, the one of the right rank among them by the full key -> c.sh->pa / pb
+// p90 order statistics of the VAD energies (:198) by ONE wave, nv <= 128: the high halves of the
+// order-preserving keys at the two ranks by repeated wave maxima; the rank's element is the one
+// holding that high half, or, when several do, the one of the right rank among them by the full
+// key -> c.sh->pa / pb
 // (a ballot radix select instead of the bitonic sorts, for p90 and the medians: 70% of the VALU of
 // those phases, but three times the SALU on the CU's shared scalar unit -- 100k clips 2.64 -> 2.71
 // ms, profiles/r05rs_ab_select.txt; removed)
@@ -857,19 +859,39 @@ __device__ __forceinline__ void p90_select_wave(const Ctx &c, int nv, int lane)
         r0 = (int)floor(vi);
         r1 = r0 + 1;
     }
-    const unsigned long long f0 = lane < nv ? dkey(c.vE[lane]) : ~0ull;
-    const unsigned long long f1 = lane + 64 < nv ? dkey(c.vE[lane + 64]) : ~0ull;
-    const unsigned h0 = (unsigned)(f0 >> 32), h1 = (unsigned)(f1 >> 32);
-    unsigned a[2] = {h0, h1};
-    wave_bitonic<2>(a, lane);
-    const unsigned ka = sorted_at<2>(a, r0), kb = sorted_at<2>(a, r1);  // the high key words at ranks r0, r1
+    const bool in0 = lane < nv, in1 = lane + 64 < nv;
+    const unsigned long long f0 = in0 ? dkey(c.vE[lane]) : 0ull;  // pads: below every real key
+    const unsigned long long f1 = in1 ? dkey(c.vE[lane + 64]) : 0ull;
+    const unsigned o0 = (unsigned)(f0 >> 32), o1 = (unsigned)(f1 >> 32);
+    // the high key words at ascending ranks r1 and r0 are the (nv - 1 - r1)-th and (nv - 1 - r0)-th
+    // largest (0-based): that many wave maxima, one occurrence removed after each (11 rounds at
+    // nv = 98; round 6 sorted all 128 slots: 28 bitonic stages over two registers, 0.31k VALU per
+    // clip for the whole selection, profiles/r06t_ab_p90.txt)
+    const int d1 = nv - 1 - r1, d0 = nv - 1 - r0;
+    unsigned h0 = o0, h1 = o1, ka = 0, kb = 0;
+    for (int t = 0;; t++) {
+        const unsigned m = wave_reduce(h0 > h1 ? h0 : h1, OpMax());
+        if (t == d1) kb = m;
+        if (t == d0) {
+            ka = m;
+            break;
+        }
+        const unsigned long long b0 = __ballot(h0 == m);
+        if (b0) {
+            if (lane == __ffsll((long long)b0) - 1) h0 = 0u;
+        } else {
+            if (lane == __ffsll((long long)__ballot(h1 == m)) - 1) h1 = 0u;
+        }
+    }
+    // the rank's element is the one holding that high word, or, when several do, the one of the
+    // right rank among them by the full key
     auto full_at = [&](int r) -> double {
-        const unsigned kh = r == r0 ? ka : kb;  // never the pad's ~0u: r < nv
-        const unsigned long long c0 = __ballot(h0 == kh), c1 = __ballot(h1 == kh);
+        const unsigned kh = r == r0 ? ka : kb;
+        const unsigned long long c0 = __ballot(in0 && o0 == kh), c1 = __ballot(in1 && o1 == kh);
         if (__popcll(c0) + __popcll(c1) == 1)
             return dkey_value(c0 ? lane_read(f0, __ffsll((long long)c0) - 1)
                                  : lane_read(f1, __ffsll((long long)c1) - 1));
-        const int rr = r - (__popcll(__ballot(h0 < kh)) + __popcll(__ballot(h1 < kh)));
+        const int rr = r - (__popcll(__ballot(in0 && o0 < kh)) + __popcll(__ballot(in1 && o1 < kh)));
         unsigned long long res = 0;
         for (int hh = 0; hh < 2; hh++) {
             unsigned long long cm = hh ? c1 : c0;
@@ -877,8 +899,8 @@ __device__ __forceinline__ void p90_select_wave(const Ctx &c, int nv, int lane)
                 const int l = __ffsll((long long)cm) - 1;
                 cm &= cm - 1;
                 const unsigned long long e = lane_read(hh ? f1 : f0, l);
-                const int lt = __popcll(__ballot(h0 == kh && f0 < e)) + __popcll(__ballot(h1 == kh && f1 < e));
-                const int eq = __popcll(__ballot(f0 == e)) + __popcll(__ballot(f1 == e));
+                const int lt = __popcll(__ballot(in0 && o0 == kh && f0 < e)) + __popcll(__ballot(in1 && o1 == kh && f1 < e));
+                const int eq = __popcll(__ballot(in0 && f0 == e)) + __popcll(__ballot(in1 && f1 == e));
                 if (rr >= lt && rr < lt + eq) res = e;
             }
         }
@@ -1687,7 +1709,12 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
             // the workgroup's critical path (p90, then the scan) runs on this one wave: it takes
             // issue priority over the co-resident workgroups' waves until the decisions are made
             __builtin_amdgcn_s_setprio(2);
-            p90_select_wave(c, nv, lane);
+            if (DSP_ABL & 64) {  // ablation only: no selection (thresholds from 0.8 x the largest energy)
+                const double mx = wave_maxd(fmax(lane < nv ? c.vE[lane] : 0.0, lane + 64 < nv ? c.vE[lane + 64] : 0.0));
+                if (lane == 0) sh->pa = sh->pb = 0.8 * mx;
+            } else {
+                p90_select_wave(c, nv, lane);
+            }
         }
         if (wid == 1) vad_noise(c, nv, lane);  // beside wave 0's p90 selection
         __syncthreads();
