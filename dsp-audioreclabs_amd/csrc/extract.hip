@@ -735,6 +735,22 @@ __device__ __forceinline__ void r1_reduce(const R1Acc &a, Shared *sh, int wid, i
         sh->red_b[wid] = wmx;
     }
 }
+// FAST: the R1 partials of each 16-lane row (DPP within the row only) -> 32 slots of LDS per
+// quantity (in the VAD energy array, unused until pass B); wave 0 combines them in clip_stats_rows
+// (round 6: every wave reduced its 64 lanes with 4 readlanes per quantity)
+__device__ __forceinline__ void r1_reduce_rows(const R1Acc &a, const Ctx &c, int wid, int lane)
+{
+    const int kmn = min(a.kmin, min((int)a.pmin.x, (int)a.pmin.y));
+    const int kmx = max(a.kmax, max((int)a.pmax.x, (int)a.pmax.y));
+    const int ks = dpp_row_reduce(a.K, OpAdd()), rmn = dpp_row_reduce(kmn, OpMin()), rmx = dpp_row_reduce(kmx, OpMax());
+    if ((lane & 15) == 0) {
+        int *rk = reinterpret_cast<int *>(c.vE);
+        const int slot = 4 * wid + (lane >> 4);
+        rk[slot] = ks;
+        rk[32 + slot] = rmn;
+        rk[64 + slot] = rmx;
+    }
+}
 // R2 of one buffer word: bit b set <=> buffer sample 32w + b is the clip's and k >= tpos (positive
 // after preprocess).  Per 16-B vector (8 samples): each pair's (k - tpos) saturated (v_pk_sub_i16),
 // the four samples of two pairs gathered by ONE v_perm as 0xFF / 0x00 bytes (selectors 8-11
@@ -832,6 +848,24 @@ __device__ __forceinline__ ClipStats clip_stats(const Shared *sh, int n, int L, 
     }
     ClipStats s;
     s.mq = uni((double)Kt / (double)n);
+    s.Mp = uni(fmax((double)kmax - s.mq, s.mq - (double)kmin));
+    s.tpos = uni((int)floor(s.mq) + 1);
+    s.t0 = uni((int)floor(s.mq + 0.5));
+    s.invMf = uni(s.Mp > 0.0 ? (float)(1.0 / s.Mp) : 0.0f);  // as dsp_extract_general (same bits)
+    s.invM2 = uni(s.Mp > 0.0 ? 1.0 / (s.Mp * s.Mp) : 0.0);   // endpoint energies (one rounding)
+    s.nv = (do_vad && n >= L) ? (n - L) / S + 1 : 0;
+    s.kneg = kmin == -32768;
+    return s;
+}
+// clip_stats of the FAST layout, by wave 0 from r1_reduce_rows's 32 row partials (one per lane)
+__device__ __forceinline__ ClipStats clip_stats_rows(const Ctx &c, int lane, int n, int L, int S, int do_vad)
+{
+    const int *rk = reinterpret_cast<const int *>(c.vE);
+    const int K = wave_sum(lane < 32 ? rk[lane] : 0);  // |K| < 2^31 (n <= 49 152 samples)
+    const int kmin = wave_min(lane < 32 ? rk[32 + lane] : 0x7fffffff);
+    const int kmax = wave_max(lane < 32 ? rk[64 + lane] : -0x7fffffff - 1);
+    ClipStats s;
+    s.mq = uni((double)K / (double)n);
     s.Mp = uni(fmax((double)kmax - s.mq, s.mq - (double)kmin));
     s.tpos = uni((int)floor(s.mq) + 1);
     s.t0 = uni((int)floor(s.mq + 0.5));
@@ -1040,17 +1074,20 @@ __device__ __forceinline__ int r4_frames(const ExtractParams &p, const Ctx &c, c
                 for (int k = 0; k < KV; k++)
                     if (vl + 16 * k == vfix) xv[k][(n - 1) & 7] = klast;
             const int jl = 8 * vl - fs;  // window index of the lane's first vector
-            auto run = [&](auto pt, auto nt) {
+            auto run = [&](auto pt, auto nt, auto ft) {
 #pragma unroll
                 for (int k = 0; k < KV; k++)
-                    if (16 * k <= vlim) frame_vec(pt, nt, xv[k], wr, jl + 128 * k, lim, ea, m0, m1);
+                    if (decltype(ft)::value || 16 * k <= vlim) frame_vec(pt, nt, xv[k], wr, jl + 128 * k, lim, ea, m0, m1);
             };
+            // a batch every lane fills (the first of an unpadded frame) runs without the per-vector
+            // lane bounds
+            const bool full = !padded && __all(vlim >= 16 * (KV - 1));
             if (padded)
-                cx.near0 ? run(BoolT<true>(), BoolT<true>()) : run(BoolT<true>(), BoolT<false>());
+                cx.near0 ? run(BoolT<true>(), BoolT<true>(), BoolT<false>()) : run(BoolT<true>(), BoolT<false>(), BoolT<false>());
             else if (cx.near0)
-                run(BoolT<false>(), BoolT<true>());
+                full ? run(BoolT<false>(), BoolT<true>(), BoolT<true>()) : run(BoolT<false>(), BoolT<true>(), BoolT<false>());
             else
-                run(BoolT<false>(), BoolT<false>());
+                full ? run(BoolT<false>(), BoolT<false>(), BoolT<true>()) : run(BoolT<false>(), BoolT<false>(), BoolT<false>());
         }
         const float E1 = dpp_row_reduce(ea.x + ea.y, OpAdd()) * sE;
         const float M1 = dpp_row_reduce(m0 + m1, OpAdd()) * sM;
@@ -1639,7 +1676,7 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     }
     if (wid == NWAVE - 1) r1_edges(r1_edge_issue(p, cur, lane), nword, lane, acc, c.wS1, c.wS2);
     MARK(R1red);
-    r1_reduce(acc, sh, wid, lane);
+    r1_reduce_rows(acc, c, wid, lane);
     __syncthreads();
     if (tid == 0 && sh->sclear) {  // the last flush's slots (every thread has read them by now)
         sh->smask = 0;
@@ -1648,7 +1685,7 @@ __device__ __forceinline__ bool clip_fast(const ExtractParams &p, const Ctx &c, 
     }
     MARK(stats);
     if (wid == 0) {  // the clip statistics once, shared through LDS
-        const ClipStats c0 = clip_stats(sh, n, L, S, p.do_vad);
+        const ClipStats c0 = clip_stats_rows(c, lane, n, L, S, p.do_vad);
         if (lane == 0) sh->cs = {c0.mq, c0.Mp, c0.invM2, c0.invMf, c0.tpos, c0.t0, c0.nv, c0.kneg};
     }
     __syncthreads();
