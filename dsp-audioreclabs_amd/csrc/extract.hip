@@ -5,11 +5,12 @@
 // registers (each thread holds EXTRACT_RREG 32-sample words):
 //   R1  registers: integer sum / min / max + exact per-word moments (sum k, sum k^2) -> LDS
 //   R2  registers: positive-sample bits per word -> LDS (the ZCR of any range is a popcount)
-//   R3  endpoint detection from the per-word summaries (+ the two partial words of each frame),
-//       p90 by a one-wave bitonic sort, double-threshold scan
+//   R3  endpoint detection from the per-word summaries (+ the two partial words of each frame;
+//       sign changes from per-segment prefixes), p90 by one wave's repeated maxima, double-
+//       threshold scan
 //   R4  windowed frames of the crop (clip-relative vectors re-read from L2, window from LDS)
 //   R5  15-d statistics
-// LDS holds only summaries, the window table and the per-frame arrays (48 992 B in the
+// LDS holds only summaries, the window table and the per-frame arrays (52 192 B in the
 // compile-time layout), so the other workgroups on the same CU compute while one waits for HBM.
 // Algorithmic traffic: 2 B/sample in + 76 B/clip out.
 //

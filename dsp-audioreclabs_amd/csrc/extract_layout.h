@@ -3,7 +3,7 @@
 // The clip itself is NOT in LDS: it is held in registers (EXTRACT_RREG 32-sample words per
 // thread) for the two passes that need every sample, and re-read from L2 by the phases that need
 // a few (crop frames, partial words at VAD frame edges).  LDS holds per-word summaries (positive-
-// sample bits, exact moments), the window table and the small per-frame arrays (~48 KB in the
+// sample bits, exact moments, sign-change prefixes), the window table and the small per-frame arrays (~52 KB in the
 // compile-time layout), so three workgroups share a CU.
 #ifndef DSP_EXTRACT_LAYOUT_H
 #define DSP_EXTRACT_LAYOUT_H
