@@ -119,9 +119,11 @@ def timed_launches(fn, n, stream):
 
 
 def assemble_result(args, world, ranks_seen, rehearsal, backend_name, C, total_frames, elapsed_x, elapsed_g,
-                    kern_ms, kern_ms_iso=None):
+                    kern_ms, kern_ms_iso=None, elapsed_gs=None, elapsed_gp=None, xchk=None):
     """The bench line (rank 0).  world > 1: ``value`` is the K steps of extraction + all-gather
-    (configs[3] as BASELINE defines it); ``value_extract_only`` the same steps without the exchange."""
+    (configs[3] as BASELINE defines it), ``elapsed_g`` the faster of the serial loop (``elapsed_gs``)
+    and the pipelined one (``elapsed_gp``: each step's gather beside the next step's extraction);
+    ``value_extract_only`` the same steps without the exchange."""
     N = 44100
     L, S, vad = args.frame_length, args.frame_shift, not args.no_vad
     K = args.steps
@@ -168,7 +170,9 @@ def assemble_result(args, world, ranks_seen, rehearsal, backend_name, C, total_f
                    "parallelism": ("dp%d (clips sharded; each step = extraction + one packed %s all-gather "
                                    "of the per-clip results)" % (world, backend_name)) if world > 1 else
                                   "dp1 (no collective)",
-                   "launch": ("python loop of the %d steps (extraction + all-gather)" % K) if world > 1 else
+                   "launch": ("python loop of the %d steps (extraction + all-gather%s)"
+                              % (K, ", pipelined" if elapsed_gp is not None and elapsed_gp <= elapsed_gs else ""))
+                             if world > 1 else
                              ("hip graph of the %d steps" % K if not args.no_graph else "python loop")},
         "roofline": roof,
     }
@@ -176,6 +180,18 @@ def assemble_result(args, world, ranks_seen, rehearsal, backend_name, C, total_f
         # the same K steps without the exchange (hip graph): what the kernel alone scales to
         result["value_extract_only"] = round(total_frames / elapsed_x, 1)
         result["ms_per_step_extract_only"] = round(elapsed_x / K * 1e3, 5)
+        if elapsed_gs is not None:
+            result["value_serial_exchange"] = round(total_frames / elapsed_gs, 1)
+            result["ms_per_step_serial_exchange"] = round(elapsed_gs / K * 1e3, 5)
+        if elapsed_gp is not None:
+            result["value_pipelined_exchange"] = round(total_frames / elapsed_gp, 1)
+            result["ms_per_step_pipelined_exchange"] = round(elapsed_gp / K * 1e3, 5)
+            result["exchange"] = ("value = the faster of two step loops, both measured in this run: serial "
+                                  "(each all-gather right after its extraction) and pipelined (step i's all-gather "
+                                  "on a second stream beside step i+1's extraction, two output buffers); both "
+                                  "extract every batch whole and gather all its rows inside the timed region")
+        if xchk is not None:
+            result["exchange_own_block_equal"] = xchk
     if rehearsal:
         result["rehearsal"] = True
         result["backend"] = backend_name
@@ -222,7 +238,7 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
-    from src.distributed import gather_rows, shard_range
+    from src.distributed import gather_rows, gather_rows_async, shard_range
     from src.pipeline import FeatureExtractor
     from src.synth import make_batch_device
 
@@ -305,7 +321,7 @@ def main():
     # N > 1: configs[3] as BASELINE defines it -- every step is the rank's extraction followed by
     # the exchange, ONE packed all-gather of every per-clip result (76 B/clip) over RCCL; launched
     # from Python (the collective is not captured), K steps between barriers
-    elapsed_g, ag = None, None
+    elapsed_g, elapsed_gs, elapsed_gp, ag, xchk = None, None, None, None, None
     if world > 1:
         def step(b):
             return gather_rows(fx(b)["rows"], args.clips)
@@ -318,7 +334,45 @@ def main():
             step(pool[i % P])
         torch.cuda.synchronize(dev)
         dist.barrier()
-        elapsed_g = time.perf_counter() - t0
+        elapsed_gs = time.perf_counter() - t0  # serial: each gather waits for its extraction
+        # pipelined (RCCL, equal blocks: every bench configuration): step i's all-gather runs on a
+        # second stream beside step i + 1's extraction; two output buffers (two extractors), and an
+        # extraction waits (on the device) for the gather that last read its buffer.  Every step
+        # still extracts its whole batch and exchanges all of its rows inside the timed region.
+        # (gloo, the one-GPU rehearsal's backend, blocks the host in every wait: serial only, unless
+        # DSP_BENCH_PIPELINE=1 rehearses the pipelined loop too.)
+        blocks = {hi - lo for lo, hi in (shard_range(args.clips, r, world) for r in range(world))}
+        if len(blocks) == 1 and (backend == "nccl" or os.environ.get("DSP_BENCH_PIPELINE") == "1"):
+            fxs = (fx, FeatureExtractor(L, S, args.window, vad, device=dev))
+            outs = [torch.empty((world * C, 19), dtype=torch.int32, device=dev) for _ in range(2)]
+            comm = torch.cuda.Stream(dev)
+            works = [None, None]
+
+            def step_ov(i):
+                j = i & 1
+                if works[j] is not None:
+                    works[j].wait()  # the extraction stream waits for gather i - 2 (no host sync)
+                rows = fxs[j](pool[i % P])["rows"]
+                comm.wait_stream(stream)
+                with torch.cuda.stream(comm):
+                    works[j] = gather_rows_async(rows, outs[j])
+                return rows
+
+            step_ov(0)
+            step_ov(1)
+            torch.cuda.synchronize(dev)
+            works = [None, None]
+            dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for i in range(K):
+                last = step_ov(i)
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            elapsed_gp = time.perf_counter() - t0
+            # the last step's gathered rows hold this rank's block as extracted
+            xchk = bool(torch.equal(outs[(K - 1) & 1][rank * C:(rank + 1) * C], last))
+            del fxs, outs
         # the all-gather alone (median of 5), for the record
         rows = fx(pool[0])["rows"]
         torch.cuda.synchronize(dev)
@@ -334,13 +388,21 @@ def main():
               "what": "every clip's packed 76-B result row (feat, start/end, n_frames, status) as written by "
                       "the kernel, one %s all_gather_into_tensor, no pack/unpack kernels" % backend_name}
     if world > 1:
-        t = torch.tensor([elapsed_x, elapsed_g, my_frames, kern_ms, kern_ms_iso], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed_x, elapsed_gs, my_frames, kern_ms, kern_ms_iso,
+                          -1.0 if elapsed_gp is None else elapsed_gp], dtype=torch.float64, device=dev)
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t.clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        elapsed_x, elapsed_g, total_frames, kern_ms = tmax[0].item(), tmax[1].item(), tsum[2].item(), tmax[3].item()
+        elapsed_x, elapsed_gs, total_frames, kern_ms = tmax[0].item(), tmax[1].item(), tsum[2].item(), tmax[3].item()
         kern_ms_iso = tmax[4].item()
+        elapsed_gp = tmax[5].item() if elapsed_gp is not None else None
+        # value: the faster of the two step loops (both measured here, both in the line)
+        elapsed_g = elapsed_gs if elapsed_gp is None else min(elapsed_gs, elapsed_gp)
+        if xchk is not None:  # every rank's own block
+            ok = torch.tensor([1 if xchk else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            xchk = bool(ok.item())
         if timed_ok is not None:  # every rank's last timed step
             ok = torch.tensor([1 if timed_ok else 0], dtype=torch.int32, device=dev)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
@@ -357,7 +419,7 @@ def main():
     result = None
     if rank == 0:
         result = assemble_result(args, world, ranks_seen, rehearsal, backend_name, C, total_frames, elapsed_x,
-                                 elapsed_g, kern_ms, kern_ms_iso)
+                                 elapsed_g, kern_ms, kern_ms_iso, elapsed_gs, elapsed_gp, xchk)
         if peaks is not None:
             r = result["roofline"]
             r["measured_read_peak_gbs"] = peaks["read_gbs"]

@@ -108,6 +108,20 @@ def gather_rows(rows, total, group=None):
     return torch.cat([out[r * m:r * m + sizes[r]] for r in range(ws)])
 
 
+def gather_rows_async(rows, out, group=None):
+    """``gather_rows`` for equal blocks into a caller-owned ``out`` [world * n, W], issued on the
+    current stream without waiting: returns the collective's work handle (``work.wait()`` makes the
+    caller's current stream wait for it).  With it the exchange of one batch can run beside the
+    extraction of the next (bench.py's N > 1 step, two output buffers)."""
+    rank, ws = world()
+    if out.shape[0] != ws * rows.shape[0] or out.shape[1:] != rows.shape[1:]:
+        raise ValueError("out must be [world * %d, ...] like rows" % rows.shape[0])
+    if ws == 1:
+        out.copy_(rows)
+        return None
+    return dist.all_gather_into_tensor(out, rows.contiguous(), group=group, async_op=True)
+
+
 def result_views(rows):
     """The per-array results as views of packed rows [B, 19] (the layout of FeatureExtractor's
     ``rows``: feat[15] as f32 bits, start, end, n_frames, status)."""
