@@ -54,6 +54,21 @@ def test_multirank_line_carries_both_values():
     r1 = m.assemble_result(args, 1, 1, False, None, 100000, 4.0e8, 0.02, None, 2.8)
     assert "value_extract_only" not in r1 and r1["value"] == round(4.0e8 / 0.02, 1)
     assert r1["config"]["parallelism"].startswith("dp1")
+    # both exchange loops timed (RCCL): value from the faster, both reported
+    r8 = m.assemble_result(args, 8, 8, False, "RCCL", 12500, 4.0e8, 0.004, 0.0045, 0.35, None, 0.005, 0.0045, True)
+    assert r8["value"] == round(4.0e8 / 0.0045, 1) and r8["ms_per_step"] == 0.45
+    assert r8["ms_per_step_serial_exchange"] == 0.5 and r8["ms_per_step_pipelined_exchange"] == 0.45
+    assert r8["exchange_own_block_equal"] is True and "pipelined" in r8["config"]["launch"]
+
+
+def test_committed_pipelined_rehearsal_line():
+    """The committed 2-rank rehearsal of both exchange loops (gloo, DSP_BENCH_PIPELINE=1)."""
+    p = os.path.join(REPO, "profiles", "r06z_rehearsal_pipelined.json")
+    with open(p) as f:
+        d = json.loads([l for l in f.read().splitlines() if l.startswith("{")][-1])
+    assert d["rehearsal"] is True and d["n_gpus"] == 2
+    assert d["exchange_own_block_equal"] is True and d["timed_outputs_equal"] is True
+    assert d["ms_per_step"] == min(d["ms_per_step_serial_exchange"], d["ms_per_step_pipelined_exchange"])
 
 
 def test_committed_rehearsal_line():
