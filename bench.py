@@ -170,8 +170,9 @@ def assemble_result(args, world, ranks_seen, rehearsal, backend_name, C, total_f
                    "parallelism": ("dp%d (clips sharded; each step = extraction + one packed %s all-gather "
                                    "of the per-clip results)" % (world, backend_name)) if world > 1 else
                                   "dp1 (no collective)",
-                   "launch": ("python loop of the %d steps (extraction + all-gather%s)"
-                              % (K, ", pipelined" if elapsed_gp is not None and elapsed_gp <= elapsed_gs else ""))
+                   "launch": ("python loop of the %d steps (%s extraction + all-gather%s)"
+                              % (K, "eager" if args.no_graph else "graph-replayed",
+                                 ", pipelined" if elapsed_gp is not None and elapsed_gp <= elapsed_gs else ""))
                              if world > 1 else
                              ("hip graph of the %d steps" % K if not args.no_graph else "python loop")},
         "roofline": roof,
@@ -323,15 +324,40 @@ def main():
     # from Python (the collective is not captured), K steps between barriers
     elapsed_g, elapsed_gs, elapsed_gp, ag, xchk = None, None, None, None, None
     if world > 1:
-        def step(b):
-            return gather_rows(fx(b)["rows"], args.clips)
-        step(pool[0])
+        def one_step_graphs(f):
+            """ext(i): step i's extraction by f on pool[i % P] -- a replay of a one-launch HIP graph
+            per batch (eager launches leave ~15 us of idle GPU per step at 12.5k clips,
+            profiles/r06z_eager_step.txt), eager with --no-graph; returns f's output rows."""
+            if args.no_graph:
+                return lambda i: f(pool[i % P])["rows"]
+            gs, rows = [], None
+            cs = torch.cuda.Stream(dev)
+            for b in pool:
+                with torch.cuda.stream(cs):  # the capture stream's own clip-queue scratch, outside the graph
+                    f(b)
+                cs.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=cs):
+                    rows = f(b)["rows"]
+                gs.append(g)
+            torch.cuda.synchronize(dev)
+
+            def ext(i):
+                gs[i % P].replay()
+                return rows
+            return ext
+
+        ext0 = one_step_graphs(fx)
+
+        def step(i):
+            return gather_rows(ext0(i), args.clips)
+        step(0)
         torch.cuda.synchronize(dev)
         dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for i in range(K):
-            step(pool[i % P])
+            step(i)
         torch.cuda.synchronize(dev)
         dist.barrier()
         elapsed_gs = time.perf_counter() - t0  # serial: each gather waits for its extraction
@@ -343,7 +369,8 @@ def main():
         # DSP_BENCH_PIPELINE=1 rehearses the pipelined loop too.)
         blocks = {hi - lo for lo, hi in (shard_range(args.clips, r, world) for r in range(world))}
         if len(blocks) == 1 and (backend == "nccl" or os.environ.get("DSP_BENCH_PIPELINE") == "1"):
-            fxs = (fx, FeatureExtractor(L, S, args.window, vad, device=dev))
+            fx2 = FeatureExtractor(L, S, args.window, vad, device=dev)
+            exts = (ext0, one_step_graphs(fx2))
             outs = [torch.empty((world * C, 19), dtype=torch.int32, device=dev) for _ in range(2)]
             comm = torch.cuda.Stream(dev)
             works = [None, None]
@@ -352,7 +379,7 @@ def main():
                 j = i & 1
                 if works[j] is not None:
                     works[j].wait()  # the extraction stream waits for gather i - 2 (no host sync)
-                rows = fxs[j](pool[i % P])["rows"]
+                rows = exts[j](i)
                 comm.wait_stream(stream)
                 with torch.cuda.stream(comm):
                     works[j] = gather_rows_async(rows, outs[j])
@@ -372,7 +399,7 @@ def main():
             elapsed_gp = time.perf_counter() - t0
             # the last step's gathered rows hold this rank's block as extracted
             xchk = bool(torch.equal(outs[(K - 1) & 1][rank * C:(rank + 1) * C], last))
-            del fxs, outs
+            del exts, fx2, outs
         # the all-gather alone (median of 5), for the record
         rows = fx(pool[0])["rows"]
         torch.cuda.synchronize(dev)
